@@ -1,0 +1,409 @@
+// heat2d_amd — Python bindings (pybind11) of the native runtime: the engine, the CPU oracle,
+// the decomposition/plan, I/O, device queries and raw-pointer kernel ops (for torch tensors).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime.h>
+
+#include "cpu_reference.h"
+#include "decomposition.h"
+#include "engine.h"
+#include "io.h"
+#include "kernels.h"
+
+namespace py = pybind11;
+using namespace h2d;
+
+namespace {
+
+py::array_t<float> to_array(const std::vector<float>& v, int64_t rows, int64_t cols) {
+  py::array_t<float> a({rows, cols});
+  std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
+  return a;
+}
+
+const float* checked_grid(const py::array_t<float, py::array::c_style | py::array::forcecast>& a, int64_t rows,
+                          int64_t cols) {
+  if (a.ndim() != 2 || a.shape(0) != rows || a.shape(1) != cols)
+    throw std::invalid_argument("expected a float32 array of shape (" + std::to_string(rows) + ", " +
+                                std::to_string(cols) + ")");
+  return a.data();
+}
+
+py::dict geom_dict(const TileGeom& g) {
+  py::dict d;
+  d["NX"] = g.NX;
+  d["NY"] = g.NY;
+  d["gx0"] = g.gx0;
+  d["gy0"] = g.gy0;
+  d["xcell"] = g.xcell;
+  d["ycell"] = g.ycell;
+  d["G"] = g.G;
+  d["PL"] = g.PL;
+  d["pitch"] = g.pitch;
+  d["srows"] = g.srows;
+  return d;
+}
+
+TileGeom geom_from(const py::dict& d) {
+  TileGeom g;
+  g.NX = d["NX"].cast<int64_t>();
+  g.NY = d["NY"].cast<int64_t>();
+  g.gx0 = d["gx0"].cast<int64_t>();
+  g.gy0 = d["gy0"].cast<int64_t>();
+  g.xcell = d["xcell"].cast<int64_t>();
+  g.ycell = d["ycell"].cast<int64_t>();
+  g.G = d["G"].cast<int64_t>();
+  g.PL = d["PL"].cast<int64_t>();
+  g.pitch = d["pitch"].cast<int64_t>();
+  g.srows = d["srows"].cast<int64_t>();
+  return g;
+}
+
+py::dict stats_dict(const RunStats& s) {
+  py::dict d;
+  d["steps_done"] = s.steps_done;
+  d["converged"] = s.converged;
+  d["residual"] = s.residual;
+  d["device_ms"] = s.device_ms;
+  d["wall_ms"] = s.wall_ms;
+  d["chunks"] = s.chunks;
+  d["exchanges"] = s.exchanges;
+  d["path"] = s.path;
+  return d;
+}
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+py::dict device_props(int dev) {
+  hipDeviceProp_t p;
+  H2D_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+  py::dict d;
+  d["name"] = std::string(p.name);
+  d["gcn_arch"] = std::string(p.gcnArchName);
+  d["major"] = p.major;
+  d["minor"] = p.minor;
+  d["total_global_mem"] = (int64_t)p.totalGlobalMem;
+  d["shared_mem_per_block"] = (int64_t)p.sharedMemPerBlock;
+  d["total_const_mem"] = (int64_t)p.totalConstMem;
+  d["regs_per_block"] = p.regsPerBlock;
+  d["warp_size"] = p.warpSize;
+  d["max_threads_per_block"] = p.maxThreadsPerBlock;
+  d["max_threads_dim"] = std::vector<int>{p.maxThreadsDim[0], p.maxThreadsDim[1], p.maxThreadsDim[2]};
+  d["max_grid_size"] = std::vector<int>{p.maxGridSize[0], p.maxGridSize[1], p.maxGridSize[2]};
+  d["multiprocessor_count"] = p.multiProcessorCount;
+  d["clock_rate_khz"] = p.clockRate;
+  d["l2_cache_size"] = p.l2CacheSize;
+  return d;
+}
+
+// Build the all-units list of a tile on the host (raw-pointer ops path).
+std::vector<Unit> all_units(const TileGeom& g, int K, int H) {
+  std::vector<Unit> v;
+  const int64_t wout = strip_out_cols(K);
+  const int64_t ns = (g.ycell + wout - 1) / wout, nq = (g.xcell + H - 1) / H;
+  for (int64_t s = 0; s < ns; ++s)
+    for (int64_t q = 0; q < nq; ++q) v.push_back(Unit{(int)s, (int)q});
+  return v;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_heat2d, m) {
+  m.doc() = "heat2d_amd native runtime (HIP/CDNA4 kernels, RCCL transport, CPU oracle)";
+
+  m.attr("FIXED") = (int)kFixed;
+  m.attr("GHOST_ZERO") = (int)kGhostZero;
+  m.attr("REF") = (int)kRef;
+  m.attr("FP32") = (int)kFp32;
+  m.attr("INIT_EXACT") = (int)kInitExact;
+  m.attr("INIT_INT32") = (int)kInitInt32;
+  m.attr("INIT_ZERO") = (int)kInitZero;
+  m.attr("CX_DOUBLE") = kCxDouble;
+  m.attr("CX_FLOAT") = kCxFloat;
+  m.attr("TRANSPORT_AUTO") = (int)kTransportAuto;
+  m.attr("TRANSPORT_LOCAL") = (int)kTransportLocal;
+  m.attr("TRANSPORT_RCCL") = (int)kTransportRccl;
+  m.attr("TRANSPORT_EXTERNAL") = (int)kTransportExternal;
+  m.attr("TEXT_GRAD") = (int)kTextGrad;
+  m.attr("TEXT_HEAT2DN") = (int)kTextHeat2dn;
+  m.attr("WAVE_COLS") = kWaveCols;
+  m.attr("MAX_K") = kMaxK;
+
+  // ---- numerics -------------------------------------------------------------------------
+  m.def("update_ref", &update_ref, "bit-exact reference cell update (c, n, s, w, e, cx, cy)");
+  m.def("update_f32", &update_f32, "fp32 FMA cell update (c, n, s, w, e, cx, cy)");
+  m.def("init_value", &init_value, py::arg("mode"), py::arg("gx"), py::arg("gy"), py::arg("NX"), py::arg("NY"));
+  m.def(
+      "init_global",
+      [](int64_t nx, int64_t ny, int init) {
+        std::vector<float> u;
+        init_global(u, nx, ny, init);
+        return to_array(u, nx, ny);
+      },
+      py::arg("nx"), py::arg("ny"), py::arg("init") = (int)kInitExact);
+  m.def(
+      "oracle_run",
+      [](int64_t nx, int64_t ny, int64_t steps, int boundary, int precision, double cx, double cy, int init,
+         bool convergence, int64_t interval, double sensitivity, bool per_x, bool per_y, py::object initial) {
+        Physics ph;
+        ph.boundary = boundary;
+        ph.precision = precision;
+        ph.cx = cx;
+        ph.cy = cy;
+        ph.periodic_x = per_x;
+        ph.periodic_y = per_y;
+        OracleResult r;
+        if (initial.is_none()) {
+          py::gil_scoped_release nogil;
+          r = oracle_run(nx, ny, steps, ph, init, convergence, interval, sensitivity, nullptr);
+        } else {
+          auto a = initial.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+          const float* p = checked_grid(a, nx, ny);
+          py::gil_scoped_release nogil;
+          r = oracle_run(nx, ny, steps, ph, init, convergence, interval, sensitivity, p);
+        }
+        py::dict d;
+        d["grid"] = to_array(r.grid, nx, ny);
+        d["steps_done"] = r.steps_done;
+        d["converged"] = r.converged;
+        d["residual"] = r.residual;
+        return d;
+      },
+      py::arg("nx"), py::arg("ny"), py::arg("steps"), py::arg("boundary") = (int)kFixed,
+      py::arg("precision") = (int)kRef, py::arg("cx") = kCxDouble, py::arg("cy") = kCxDouble,
+      py::arg("init") = (int)kInitExact, py::arg("convergence") = false, py::arg("interval") = 20,
+      py::arg("sensitivity") = 0.1, py::arg("periodic_x") = false, py::arg("periodic_y") = false,
+      py::arg("initial") = py::none());
+
+  // ---- decomposition ----------------------------------------------------------------------
+  py::class_<Decomposition>(m, "Decomposition")
+      .def(py::init<int64_t, int64_t, int, int, bool, bool>(), py::arg("nx"), py::arg("ny"), py::arg("gridx"),
+           py::arg("gridy"), py::arg("periodic_x") = false, py::arg("periodic_y") = false)
+      .def_readonly("NX", &Decomposition::NX)
+      .def_readonly("NY", &Decomposition::NY)
+      .def_readonly("gridx", &Decomposition::gridx)
+      .def_readonly("gridy", &Decomposition::gridy)
+      .def_readonly("xstart", &Decomposition::xstart)
+      .def_readonly("xcount", &Decomposition::xcount)
+      .def_readonly("ystart", &Decomposition::ystart)
+      .def_readonly("ycount", &Decomposition::ycount)
+      .def("nranks", &Decomposition::nranks)
+      .def("px_of", &Decomposition::px_of)
+      .def("py_of", &Decomposition::py_of)
+      .def("rank_of", &Decomposition::rank_of)
+      .def("neighbor", &Decomposition::neighbor)
+      .def("max_halo_depth", &Decomposition::max_halo_depth)
+      .def("tile", [](const Decomposition& d, int rank, int64_t G) { return geom_dict(d.tile(rank, G)); })
+      .def("plan",
+           [](const Decomposition& d, int rank, int64_t G, int K) {
+             ExchangePlan p = make_plan(d, rank, d.tile(rank, G), K);
+             py::list out;
+             for (int dir = 0; dir < kNumDirs; ++dir) {
+               py::dict e;
+               e["peer"] = p.peer[dir];
+               e["send"] = py::make_tuple(p.send_rect[dir].r0, p.send_rect[dir].c0, p.send_rect[dir].rows,
+                                          p.send_rect[dir].cols);
+               e["recv"] = py::make_tuple(p.recv_rect[dir].r0, p.recv_rect[dir].c0, p.recv_rect[dir].rows,
+                                          p.recv_rect[dir].cols);
+               e["send_off"] = p.send_off[dir];
+               e["recv_off"] = p.recv_off[dir];
+               out.append(e);
+             }
+             return out;
+           })
+      .def("__repr__", [](const Decomposition& d) { return describe(d); });
+  m.def("tile_geom", [](int64_t nx, int64_t ny, int64_t G) { return geom_dict(make_tile_geom(nx, ny, 0, 0, nx, ny, G)); },
+        py::arg("nx"), py::arg("ny"), py::arg("G"));
+  m.attr("DIR_NAMES") = std::vector<std::string>{"N", "S", "W", "E", "NW", "NE", "SW", "SE"};
+  m.attr("DIR_OPP") = std::vector<int>(kDirOpp, kDirOpp + kNumDirs);
+
+  // ---- engine -----------------------------------------------------------------------------
+  py::class_<Engine>(m, "Engine")
+      .def(py::init([](int64_t nx, int64_t ny, int gridx, int gridy, bool per_x, bool per_y, int boundary,
+                       int precision, int init, double cx, double cy, int tblock, int rows_per_wave, bool convergence,
+                       int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
+                       bool overlap, bool small_grid_lds, bool naive) {
+             EngineOptions o;
+             o.nx = nx;
+             o.ny = ny;
+             o.gridx = gridx;
+             o.gridy = gridy;
+             o.periodic_x = per_x;
+             o.periodic_y = per_y;
+             o.boundary = boundary;
+             o.precision = precision;
+             o.init = init;
+             o.cx = cx;
+             o.cy = cy;
+             o.tblock = tblock;
+             o.rows_per_wave = rows_per_wave;
+             o.convergence = convergence;
+             o.interval = interval;
+             o.sensitivity = sensitivity;
+             o.device = device;
+             o.ranks = ranks;
+             o.transport = transport;
+             o.overlap = overlap;
+             o.small_grid_lds = small_grid_lds;
+             o.naive = naive;
+             return new Engine(o);
+           }),
+           py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
+           py::arg("periodic_y") = false, py::arg("boundary") = (int)kFixed, py::arg("precision") = (int)kRef,
+           py::arg("init") = (int)kInitExact, py::arg("cx") = kCxDouble, py::arg("cy") = kCxDouble,
+           py::arg("tblock") = 8, py::arg("rows_per_wave") = 0, py::arg("convergence") = false,
+           py::arg("interval") = 20, py::arg("sensitivity") = 0.1, py::arg("device") = 0,
+           py::arg("ranks") = std::vector<int>{}, py::arg("transport") = (int)kTransportAuto,
+           py::arg("overlap") = true, py::arg("small_grid_lds") = true, py::arg("naive") = false)
+      .def("num_tiles", &Engine::num_tiles)
+      .def("tile_rank", &Engine::tile_rank)
+      .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })
+      .def("halo_depth", &Engine::halo_depth)
+      .def("has_exchange", &Engine::has_exchange)
+      .def("on_gpu", &Engine::on_gpu)
+      .def("rows_per_wave", &Engine::rows_per_wave)
+      .def("steps_done", &Engine::steps_done)
+      .def("set_steps_done", &Engine::set_steps_done)
+      .def("stream_handle", &Engine::stream_handle)
+      .def_static("rccl_unique_id", []() { return py::bytes(Engine::rccl_unique_id()); })
+      .def("init_rccl", [](Engine& e, py::bytes id, int n, int r) {
+        std::string s = id;
+        py::gil_scoped_release nogil;
+        e.init_rccl(s, n, r);
+      })
+      .def("rccl_ready", &Engine::rccl_ready)
+      .def("run",
+           [](Engine& e, int64_t steps) {
+             RunStats s;
+             {
+               py::gil_scoped_release nogil;
+               s = e.run(steps);
+             }
+             return stats_dict(s);
+           })
+      .def("next_chunk",
+           [](const Engine& e, int64_t done, int64_t total) {
+             bool check = false;
+             const int k = e.next_chunk(done, total, &check);
+             return py::make_tuple(k, check);
+           })
+      .def("advance", &Engine::advance, py::arg("k"), py::arg("residual") = false,
+           py::call_guard<py::gil_scoped_release>())
+      .def("exchange_local", &Engine::exchange_local, py::call_guard<py::gil_scoped_release>())
+      .def("local_residual", &Engine::local_residual, py::call_guard<py::gil_scoped_release>())
+      .def("send_count", &Engine::send_count)
+      .def("recv_count", &Engine::recv_count)
+      .def("plan_info", &Engine::plan_info)
+      .def("pack", &Engine::pack, py::call_guard<py::gil_scoped_release>())
+      .def("unpack", &Engine::unpack, py::call_guard<py::gil_scoped_release>())
+      .def("rollback", &Engine::rollback)
+      .def("download",
+           [](const Engine& e, int t) {
+             const TileGeom g = e.geom(t);
+             std::vector<float> v;
+             {
+               py::gil_scoped_release nogil;
+               v = e.download(t);
+             }
+             return to_array(v, g.xcell, g.ycell);
+           })
+      .def("upload",
+           [](Engine& e, int t, py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+             const TileGeom g = e.geom(t);
+             e.upload(t, checked_grid(a, g.xcell, g.ycell));
+           })
+      .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>());
+
+  // ---- I/O ---------------------------------------------------------------------------------
+  m.def("binary_create", &binary_create);
+  m.def("binary_write_tile", [](const std::string& path, int64_t NX, int64_t NY, int64_t gx0, int64_t gy0,
+                                py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+    if (a.ndim() != 2) throw std::invalid_argument("tile must be 2-D");
+    binary_write_tile(path, NX, NY, gx0, gy0, a.shape(0), a.shape(1), a.data());
+  });
+  m.def("binary_read", [](const std::string& path, int64_t NX, int64_t NY) {
+    return to_array(binary_read(path, NX, NY), NX, NY);
+  });
+  m.def("binary_to_text", &binary_to_text, py::call_guard<py::gil_scoped_release>());
+  m.def("format_text", [](py::array_t<float, py::array::c_style | py::array::forcecast> a, int style) {
+    if (a.ndim() != 2) throw std::invalid_argument("grid must be 2-D");
+    return py::bytes(format_text(a.data(), a.shape(0), a.shape(1), style));
+  });
+
+  // ---- devices -----------------------------------------------------------------------------
+  m.def("device_count", &device_count);
+  m.def("device_props", &device_props);
+
+  // ---- raw-pointer kernel ops (torch tensors laid out as TileGeom storage) ---------------
+  m.def(
+      "op_init",
+      [](uintptr_t base, const py::dict& geom, int init, uintptr_t stream) {
+        launch_init(geom_from(geom), reinterpret_cast<float*>(base), init, reinterpret_cast<hipStream_t>(stream));
+      },
+      py::arg("base"), py::arg("geom"), py::arg("init"), py::arg("stream") = 0);
+  m.def(
+      "op_stream",
+      [](uintptr_t src, uintptr_t dst, const py::dict& geom, int K, int precision, int boundary, double cx, double cy,
+         bool per_x, bool per_y, int H, uintptr_t partials, uintptr_t stream) {
+        const TileGeom g = geom_from(geom);
+        if (!stream_k_supported(K)) throw std::invalid_argument("unsupported K");
+        if (K > g.G) throw std::invalid_argument("K exceeds the tile's ghost depth");
+        if (H <= 0) H = 64;
+        std::vector<Unit> u = all_units(g, K, H);
+        Unit* du = nullptr;
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+        H2D_HIP_CHECK(hipMalloc(&du, u.size() * sizeof(Unit)));
+        H2D_HIP_CHECK(hipMemcpy(du, u.data(), u.size() * sizeof(Unit), hipMemcpyHostToDevice));
+        StreamArgs a;
+        a.src = reinterpret_cast<const float*>(src);
+        a.dst = reinterpret_cast<float*>(dst);
+        a.units = du;
+        a.nunits = (int)u.size();
+        a.H = H;
+        a.R = (int)lead_cols(K);
+        a.wout = (int)strip_out_cols(K);
+        a.pitch = g.pitch;
+        a.G = g.G;
+        a.PL = g.PL;
+        a.xcell = g.xcell;
+        a.ycell = g.ycell;
+        a.gx0 = g.gx0;
+        a.gy0 = g.gy0;
+        a.NX = g.NX;
+        a.NY = g.NY;
+        a.cx = cx;
+        a.cy = cy;
+        a.fixed = boundary == kFixed;
+        a.per_x = per_x;
+        a.per_y = per_y;
+        a.partials = reinterpret_cast<double*>(partials);
+        launch_stream(a, K, precision, partials != 0, s);
+        H2D_HIP_CHECK(hipStreamSynchronize(s));
+        H2D_HIP_CHECK(hipFree(du));
+        return (int)u.size();
+      },
+      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("K"), py::arg("precision") = (int)kRef,
+      py::arg("boundary") = (int)kFixed, py::arg("cx") = kCxDouble, py::arg("cy") = kCxDouble,
+      py::arg("periodic_x") = false, py::arg("periodic_y") = false, py::arg("H") = 64, py::arg("partials") = 0,
+      py::arg("stream") = 0);
+  m.def(
+      "op_naive",
+      [](uintptr_t src, uintptr_t dst, const py::dict& geom, int precision, int boundary, double cx, double cy,
+         bool per_x, bool per_y, uintptr_t stream) {
+        launch_naive_step(geom_from(geom), reinterpret_cast<const float*>(src), reinterpret_cast<float*>(dst),
+                          precision, boundary, cx, cy, per_x, per_y, reinterpret_cast<hipStream_t>(stream));
+      },
+      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("precision") = (int)kRef,
+      py::arg("boundary") = (int)kFixed, py::arg("cx") = kCxDouble, py::arg("cy") = kCxDouble,
+      py::arg("periodic_x") = false, py::arg("periodic_y") = false, py::arg("stream") = 0);
+  m.def("stream_k_supported", &stream_k_supported);
+  m.def("lds_solver_fits", &lds_solver_fits);
+  m.def("lead_cols", &lead_cols);
+  m.def("strip_out_cols", &strip_out_cols);
+}

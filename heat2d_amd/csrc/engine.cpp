@@ -1,0 +1,672 @@
+// heat2d_amd — native solver engine (see engine.h).
+#include "engine.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+#define H2D_NCCL_CHECK(call)                                                                             \
+  do {                                                                                                   \
+    ncclResult_t _r = (call);                                                                            \
+    if (_r != ncclSuccess)                                                                               \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(_r) + " at " + __FILE__ + \
+                               ":" + std::to_string(__LINE__) + ": " #call);                            \
+  } while (0)
+
+namespace h2d {
+
+namespace {
+template <class T>
+T* dmalloc(size_t n) {
+  T* p = nullptr;
+  if (n == 0) n = 1;
+  H2D_HIP_CHECK(hipMalloc(&p, n * sizeof(T)));
+  return p;
+}
+}  // namespace
+
+Engine::Engine(const EngineOptions& o) : opt_(o) {
+  dec_ = Decomposition(o.nx, o.ny, o.gridx, o.gridy, o.periodic_x, o.periodic_y);
+  if (o.tblock < 1) throw std::invalid_argument("tblock must be >= 1");
+  if (o.convergence && o.interval < 1) throw std::invalid_argument("interval must be >= 1");
+  std::vector<int> ranks = o.ranks;
+  if (ranks.empty())
+    for (int r = 0; r < dec_.nranks(); ++r) ranks.push_back(r);
+  for (int r : ranks)
+    if (r < 0 || r >= dec_.nranks()) throw std::invalid_argument("rank out of range");
+
+  // Halo / temporal-block depth: bounded by the smallest tile on exchanged dimensions.
+  int64_t G = o.tblock;
+  G = std::min<int64_t>(G, dec_.max_halo_depth());
+  if (on_gpu()) {
+    while (G > 1 && !stream_k_supported((int)G)) --G;
+  }
+  G_ = (int)std::max<int64_t>(1, G);
+
+  bool any_peer = false;
+  for (int r : ranks)
+    for (int d = 0; d < kNumDirs; ++d)
+      if (dec_.neighbor(r, d) >= 0) any_peer = true;
+  // Peers of non-local ranks also matter (a rank whose only neighbour is remote).
+  has_exchange_ = any_peer;
+
+  transport_ = o.transport;
+  if (transport_ == kTransportAuto) transport_ = ((int)ranks.size() == dec_.nranks()) ? kTransportLocal : kTransportRccl;
+  if (transport_ == kTransportLocal && (int)ranks.size() != dec_.nranks())
+    throw std::invalid_argument("local transport needs every tile in this process");
+  if (transport_ == kTransportRccl && ranks.size() != 1) throw std::invalid_argument("RCCL transport: one tile per process");
+  if (transport_ == kTransportRccl && !on_gpu()) throw std::invalid_argument("RCCL transport needs a GPU");
+
+  if (on_gpu()) {
+    H2D_HIP_CHECK(hipSetDevice(o.device));
+    H2D_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+    H2D_HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+    H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
+    H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+    H2D_HIP_CHECK(hipEventCreate(&ev_t0_));
+    H2D_HIP_CHECK(hipEventCreate(&ev_t1_));
+    d_resid_ = dmalloc<double>(ranks.size() + 1);
+    H2D_HIP_CHECK(hipHostMalloc(&h_resid_, sizeof(double) * (ranks.size() + 1)));
+    d_lds_steps_ = dmalloc<long long>(1);
+  }
+
+  for (int r : ranks) {
+    Tile t;
+    t.rank = r;
+    t.g = dec_.tile(r, G_);
+    const size_t n = (size_t)t.g.elems();
+    if (on_gpu()) {
+      for (int b = 0; b < 2; ++b) {
+        t.buf[b] = dmalloc<float>(n);
+        H2D_HIP_CHECK(hipMemsetAsync(t.buf[b], 0, n * sizeof(float), compute_));
+      }
+      launch_init(t.g, t.buf[0], o.init, compute_);
+    } else {
+      for (int b = 0; b < 2; ++b) {
+        t.host[b].assign(n, 0.0f);
+        t.buf[b] = t.host[b].data();
+        t.scratch[b].assign(n, 0.0f);
+      }
+      cpu_tile_init(t.g, t.buf[0], o.init);
+    }
+    tiles_.push_back(std::move(t));
+  }
+  if (on_gpu()) {
+    // Build every unit list (and size the residual partials) up front: nothing is
+    // allocated inside the time loop.
+    for (int t = 0; t < (int)tiles_.size(); ++t) {
+      Tile& tl = tiles_[t];
+      tl.pcap = 256;
+      tl.partials = dmalloc<double>(256);
+      for (int K = 1; K <= G_; ++K)
+        if (stream_k_supported(K)) units(t, K);
+    }
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+  }
+}
+
+Engine::~Engine() {
+  if (rccl_comm_) ncclCommDestroy((ncclComm_t)rccl_comm_);
+  if (!on_gpu()) {
+    for (auto& kv : local_descs_) delete[] std::get<0>(kv.second);
+    return;
+  }
+  hipDeviceSynchronize();
+  for (auto& t : tiles_)
+    for (int b = 0; b < 2; ++b) hipFree(t.buf[b]);
+  for (auto& kv : units_) {
+    hipFree(kv.second.d_all);
+    hipFree(kv.second.d_interior);
+    hipFree(kv.second.d_boundary);
+  }
+  for (auto* m : {&local_descs_, &pack_descs_, &unpack_descs_})
+    for (auto& kv : *m) hipFree(std::get<0>(kv.second));
+  for (auto& t : tiles_) hipFree(t.partials);
+  hipFree(d_resid_);
+  hipHostFree(h_resid_);
+  hipFree(d_lds_steps_);
+  hipFree(d_send_);
+  hipFree(d_recv_);
+  hipEventDestroy(ev_ready_);
+  hipEventDestroy(ev_halo_);
+  hipEventDestroy(ev_t0_);
+  hipEventDestroy(ev_t1_);
+  hipStreamDestroy(compute_);
+  hipStreamDestroy(comm_);
+}
+
+void Engine::check_tile(int t) const {
+  if (t < 0 || t >= (int)tiles_.size()) throw std::out_of_range("tile index");
+}
+
+int Engine::rows_per_wave(int K) const {
+  if (opt_.rows_per_wave > 0) return opt_.rows_per_wave;
+  // Enough waves to fill 256 CUs × ~8 waves while keeping the K-row cone overhead
+  // ((K-1)/H) small: H in [16, 256].
+  int64_t waves_wanted = 2048;
+  int64_t total_strips = 0, max_rows = 1;
+  for (const Tile& t : tiles_) {
+    total_strips += (t.g.ycell + strip_out_cols(K) - 1) / strip_out_cols(K);
+    max_rows = std::max(max_rows, t.g.xcell);
+  }
+  int64_t segs = std::max<int64_t>(1, waves_wanted / std::max<int64_t>(1, total_strips));
+  int64_t H = (max_rows + segs - 1) / segs;
+  H = std::max<int64_t>(H, std::max<int64_t>(16, 4 * K));
+  H = std::min<int64_t>(H, 256);
+  return (int)H;
+}
+
+const Engine::UnitLists& Engine::units(int t, int K) {
+  auto key = std::make_pair(t, K);
+  auto it = units_.find(key);
+  if (it != units_.end()) return it->second;
+  const Tile& tl = tiles_[t];
+  const TileGeom& g = tl.g;
+  UnitLists L;
+  L.H = rows_per_wave(K);
+  const int64_t wout = strip_out_cols(K);
+  const int64_t nstrips = (g.ycell + wout - 1) / wout;
+  const int64_t nsegs = (g.xcell + L.H - 1) / L.H;
+  if (nstrips * nsegs > (1LL << 30)) throw std::runtime_error("too many work units");
+  std::array<bool, kNumDirs> peer;
+  for (int d = 0; d < kNumDirs; ++d) peer[d] = dec_.neighbor(tl.rank, d) >= 0;
+  std::vector<Unit> all, in, bd;
+  for (int64_t s = 0; s < nstrips; ++s) {
+    const int64_t y0 = s * wout, y1 = std::min(g.ycell, y0 + wout);
+    const bool left = y0 - K < 0, right = y1 + K > g.ycell;
+    for (int64_t q = 0; q < nsegs; ++q) {
+      const int64_t x0 = q * L.H, x1 = std::min(g.xcell, x0 + L.H);
+      const bool top = x0 - K < 0, bot = x1 + K > g.xcell;
+      const bool needs_halo = (top && peer[kN]) || (bot && peer[kS]) || (left && peer[kW]) || (right && peer[kE]) ||
+                              (top && left && peer[kNW]) || (top && right && peer[kNE]) ||
+                              (bot && left && peer[kSW]) || (bot && right && peer[kSE]);
+      Unit u{(int)s, (int)q};
+      all.push_back(u);
+      (needs_halo ? bd : in).push_back(u);
+    }
+  }
+  L.n_all = (int)all.size();
+  L.n_interior = (int)in.size();
+  L.n_boundary = (int)bd.size();
+  if (on_gpu()) {
+    L.d_all = dmalloc<Unit>(all.size());
+    L.d_interior = dmalloc<Unit>(in.size());
+    L.d_boundary = dmalloc<Unit>(bd.size());
+    H2D_HIP_CHECK(hipMemcpy(L.d_all, all.data(), all.size() * sizeof(Unit), hipMemcpyHostToDevice));
+    if (!in.empty()) H2D_HIP_CHECK(hipMemcpy(L.d_interior, in.data(), in.size() * sizeof(Unit), hipMemcpyHostToDevice));
+    if (!bd.empty()) H2D_HIP_CHECK(hipMemcpy(L.d_boundary, bd.data(), bd.size() * sizeof(Unit), hipMemcpyHostToDevice));
+    Tile& tw = tiles_[t];
+    if ((int64_t)all.size() > tw.pcap) {
+      H2D_HIP_CHECK(hipDeviceSynchronize());
+      hipFree(tw.partials);
+      tw.pcap = std::max<int64_t>((int64_t)all.size(), 256);
+      tw.partials = dmalloc<double>((size_t)tw.pcap);
+    }
+  }
+  return units_.emplace(key, L).first->second;
+}
+
+void Engine::launch_chunk_tile(int t, int K, bool residual, int which) {
+  Tile& tl = tiles_[t];
+  const TileGeom& g = tl.g;
+  const UnitLists& L = units(t, K);
+  StreamArgs a;
+  a.src = tl.buf[tl.cur];
+  a.dst = tl.buf[1 - tl.cur];
+  a.H = L.H;
+  a.R = (int)lead_cols(K);
+  a.wout = (int)strip_out_cols(K);
+  a.pitch = g.pitch;
+  a.G = g.G;
+  a.PL = g.PL;
+  a.xcell = g.xcell;
+  a.ycell = g.ycell;
+  a.gx0 = g.gx0;
+  a.gy0 = g.gy0;
+  a.NX = g.NX;
+  a.NY = g.NY;
+  a.cx = opt_.cx;
+  a.cy = opt_.cy;
+  a.fixed = opt_.boundary == kFixed;
+  a.per_x = opt_.periodic_x;
+  a.per_y = opt_.periodic_y;
+  a.partials = tl.partials;
+  if (which == 0) {
+    a.units = L.d_all;
+    a.nunits = L.n_all;
+  } else if (which == 1) {
+    a.units = L.d_interior;
+    a.nunits = L.n_interior;
+  } else {
+    a.units = L.d_boundary;
+    a.nunits = L.n_boundary;
+    a.partials = tl.partials + L.n_interior;
+  }
+  launch_stream(a, K, opt_.precision, residual, compute_);
+  if (residual && which != 1) {
+    // Deterministic reduction of this tile's per-wave partials into d_resid_[t].
+    launch_reduce_sum(tl.partials, L.n_all, d_resid_ + t, compute_);
+  }
+}
+
+int Engine::next_chunk(int64_t done, int64_t total, bool* check) const {
+  *check = false;
+  const int64_t remaining = total - done;
+  if (remaining <= 0) return 0;
+  int64_t k = std::min<int64_t>(G_, remaining);
+  if (opt_.convergence) {
+    const int64_t next_check = (done / opt_.interval + 1) * opt_.interval;
+    if (done + 1 == next_check) {
+      *check = true;
+      return 1;
+    }
+    k = std::min<int64_t>(k, next_check - 1 - done);
+  }
+  if (on_gpu() && !opt_.naive)
+    while (k > 1 && !stream_k_supported((int)k)) --k;
+  if (opt_.naive) k = 1;
+  return (int)std::max<int64_t>(1, k);
+}
+
+CopyDesc* Engine::local_descs(int K, int& n, int64_t& maxe) {
+  // Tile-to-tile copies: peer's owned edge (its current buffer) -> my ghost ring.
+  const int parity = tiles_[0].cur;
+  auto key = std::make_pair(K, parity);
+  auto it = local_descs_.find(key);
+  if (it == local_descs_.end()) {
+    std::vector<CopyDesc> v;
+    int64_t me = 0;
+    std::map<int, int> tile_of_rank;
+    for (int t = 0; t < (int)tiles_.size(); ++t) tile_of_rank[tiles_[t].rank] = t;
+    for (int t = 0; t < (int)tiles_.size(); ++t) {
+      Tile& T = tiles_[t];
+      ExchangePlan p = make_plan(dec_, T.rank, T.g, K);
+      for (int d = 0; d < kNumDirs; ++d) {
+        if (p.peer[d] < 0) continue;
+        const Tile& U = tiles_[tile_of_rank.at(p.peer[d])];
+        ExchangePlan q = make_plan(dec_, U.rank, U.g, K);
+        const Rect& s = q.send_rect[kDirOpp[d]];
+        const Rect& r = p.recv_rect[d];
+        if (s.rows != r.rows || s.cols != r.cols) throw std::logic_error("halo shape mismatch");
+        v.push_back(CopyDesc{U.buf[U.cur] + U.g.idx(s.r0, s.c0), T.buf[T.cur] + T.g.idx(r.r0, r.c0), U.g.pitch,
+                             T.g.pitch, r.rows, r.cols});
+        me = std::max(me, r.count());
+      }
+    }
+    CopyDesc* dd = nullptr;
+    if (on_gpu() && !v.empty()) {
+      dd = dmalloc<CopyDesc>(v.size());
+      H2D_HIP_CHECK(hipMemcpy(dd, v.data(), v.size() * sizeof(CopyDesc), hipMemcpyHostToDevice));
+    } else if (!on_gpu()) {
+      // CPU: keep the host descriptors alive in a heap block.
+      dd = new CopyDesc[v.size() ? v.size() : 1];
+      std::copy(v.begin(), v.end(), dd);
+    }
+    it = local_descs_.emplace(key, std::make_tuple(dd, (int)v.size(), me)).first;
+  }
+  n = std::get<1>(it->second);
+  maxe = std::get<2>(it->second);
+  return std::get<0>(it->second);
+}
+
+void Engine::exchange_local(int k) {
+  if (!has_exchange_) return;
+  int n = 0;
+  int64_t me = 0;
+  CopyDesc* d = local_descs(k, n, me);
+  if (n == 0) return;
+  if (on_gpu()) {
+    launch_copy_rects(d, n, me, compute_);
+  } else {
+    cpu_copy_rects(std::vector<CopyDesc>(d, d + n));
+  }
+}
+
+void Engine::do_exchange_async(int K) {
+  // Runs on comm_ after ev_ready_.
+  if (transport_ == kTransportLocal) {
+    int n = 0;
+    int64_t me = 0;
+    CopyDesc* d = local_descs(K, n, me);
+    launch_copy_rects(d, n, me, comm_);
+    return;
+  }
+  if (transport_ != kTransportRccl) throw std::logic_error("do_exchange_async: transport");
+  if (!rccl_comm_) throw std::runtime_error("RCCL transport selected but init_rccl() was not called");
+  Tile& T = tiles_[0];
+  ExchangePlan p = make_plan(dec_, T.rank, T.g, K);
+  if (p.send_total > stage_cap_ || p.recv_total > stage_cap_) {
+    H2D_HIP_CHECK(hipStreamSynchronize(comm_));
+    hipFree(d_send_);
+    hipFree(d_recv_);
+    stage_cap_ = std::max(p.send_total, p.recv_total);
+    d_send_ = dmalloc<float>((size_t)stage_cap_);
+    d_recv_ = dmalloc<float>((size_t)stage_cap_);
+    for (auto* m : {&pack_descs_, &unpack_descs_}) {
+      for (auto& kv : *m) hipFree(std::get<0>(kv.second));
+      m->clear();
+    }
+  }
+  auto key = std::make_pair(K, T.cur);
+  auto ip = pack_descs_.find(key);
+  if (ip == pack_descs_.end()) {
+    std::vector<CopyDesc> pv, uv;
+    plan_pack_descs(p, T.g, T.buf[T.cur], d_send_, pv);
+    plan_unpack_descs(p, T.g, T.buf[T.cur], d_recv_, uv);
+    int64_t me = 0;
+    for (auto& c : pv) me = std::max(me, c.rows * c.cols);
+    CopyDesc* dp = dmalloc<CopyDesc>(pv.size());
+    CopyDesc* du = dmalloc<CopyDesc>(uv.size());
+    if (!pv.empty()) H2D_HIP_CHECK(hipMemcpy(dp, pv.data(), pv.size() * sizeof(CopyDesc), hipMemcpyHostToDevice));
+    if (!uv.empty()) H2D_HIP_CHECK(hipMemcpy(du, uv.data(), uv.size() * sizeof(CopyDesc), hipMemcpyHostToDevice));
+    ip = pack_descs_.emplace(key, std::make_tuple(dp, (int)pv.size(), me)).first;
+    unpack_descs_.emplace(key, std::make_tuple(du, (int)uv.size(), me));
+  }
+  auto iu = unpack_descs_.find(key);
+  launch_copy_rects(std::get<0>(ip->second), std::get<1>(ip->second), std::get<2>(ip->second), comm_);
+  ncclComm_t comm = (ncclComm_t)rccl_comm_;
+  H2D_NCCL_CHECK(ncclGroupStart());
+  // Send segment d to peer[d]; receive the peer's matching segment into ghost side opp(d)
+  // from peer[opp(d)].  Posting both in direction order keeps per-peer FIFO matching
+  // correct even when one peer is the neighbour on several sides (periodic, 2-wide grids).
+  for (int d = 0; d < kNumDirs; ++d) {
+    if (p.peer[d] < 0 || p.send_rect[d].count() == 0) continue;
+    H2D_NCCL_CHECK(ncclSend(d_send_ + p.send_off[d], (size_t)p.send_rect[d].count(), ncclFloat, p.peer[d], comm, comm_));
+  }
+  for (int d = 0; d < kNumDirs; ++d) {
+    const int g = kDirOpp[d];
+    if (p.peer[g] < 0 || p.recv_rect[g].count() == 0) continue;
+    H2D_NCCL_CHECK(ncclRecv(d_recv_ + p.recv_off[g], (size_t)p.recv_rect[g].count(), ncclFloat, p.peer[g], comm, comm_));
+  }
+  H2D_NCCL_CHECK(ncclGroupEnd());
+  launch_copy_rects(std::get<0>(iu->second), std::get<1>(iu->second), std::get<2>(iu->second), comm_);
+}
+
+void Engine::advance(int k, bool residual) {
+  if (k < 1 || k > G_) throw std::invalid_argument("advance: chunk size must be in [1, halo depth]");
+  for (int t = 0; t < (int)tiles_.size(); ++t) {
+    Tile& tl = tiles_[t];
+    if (on_gpu()) {
+      if (opt_.naive) {
+        if (k != 1) throw std::invalid_argument("naive path advances one step at a time");
+        launch_naive_step(tl.g, tl.buf[tl.cur], tl.buf[1 - tl.cur], opt_.precision, opt_.boundary, opt_.cx, opt_.cy,
+                          opt_.periodic_x, opt_.periodic_y, compute_);
+        if (residual) {
+          const int np = 256;
+          launch_tile_residual(tl.g, tl.buf[1 - tl.cur], tl.buf[tl.cur], tl.partials, np, compute_);
+          launch_reduce_sum(tl.partials, np, d_resid_ + t, compute_);
+        }
+      } else {
+        launch_chunk_tile(t, k, residual, 0);
+      }
+    } else {
+      Physics ph;
+      ph.boundary = opt_.boundary;
+      ph.precision = opt_.precision;
+      ph.cx = opt_.cx;
+      ph.cy = opt_.cy;
+      ph.periodic_x = opt_.periodic_x;
+      ph.periodic_y = opt_.periodic_y;
+      tl.last_resid = cpu_tile_advance(tl.g, ph, tl.buf[tl.cur], tl.buf[1 - tl.cur], k, tl.scratch[0].data(),
+                                       tl.scratch[1].data(), residual);
+    }
+    tl.cur = 1 - tl.cur;
+  }
+}
+
+double Engine::local_residual() {
+  double s = 0.0;
+  if (on_gpu()) {
+    H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, sizeof(double) * tiles_.size(), hipMemcpyDeviceToHost, compute_));
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    for (size_t t = 0; t < tiles_.size(); ++t) s += h_resid_[t];
+  } else {
+    for (const Tile& t : tiles_) s += t.last_resid;
+  }
+  return s;
+}
+
+double Engine::finish_residual() {
+  if (on_gpu() && rccl_comm_) {
+    // Local sum over tiles (one tile under RCCL) -> all-reduce across ranks on the compute stream.
+    H2D_NCCL_CHECK(ncclAllReduce(d_resid_, d_resid_ + tiles_.size(), 1, ncclDouble, ncclSum, (ncclComm_t)rccl_comm_,
+                                 compute_));
+    H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_ + tiles_.size(), sizeof(double), hipMemcpyDeviceToHost, compute_));
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    return h_resid_[0];
+  }
+  return local_residual();
+}
+
+void Engine::rollback() {
+  for (Tile& t : tiles_) t.cur = 1 - t.cur;
+}
+
+RunStats Engine::run(int64_t steps) {
+  if (transport_ == kTransportExternal && has_exchange_)
+    throw std::runtime_error("external transport: drive the loop from the caller");
+  if (transport_ == kTransportRccl && has_exchange_ && !rccl_comm_)
+    throw std::runtime_error("RCCL transport selected but init_rccl() was not called");
+  RunStats st;
+  const auto w0 = std::chrono::steady_clock::now();
+  const int64_t target = steps_done_ + steps;
+
+  if (!on_gpu()) {
+    st.path = "cpu";
+    while (steps_done_ < target) {
+      bool check = false;
+      const int k = next_chunk(steps_done_, target, &check);
+      if (has_exchange_) {
+        exchange_local(k);
+        ++st.exchanges;
+      }
+      advance(k, check);
+      ++st.chunks;
+      if (check) {
+        st.residual = local_residual();
+        if (st.residual < opt_.sensitivity) {
+          rollback();
+          st.converged = true;
+          break;
+        }
+      }
+      steps_done_ += k;
+    }
+    st.steps_done = steps_done_;
+    st.wall_ms = st.device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+    return st;
+  }
+
+  H2D_HIP_CHECK(hipEventRecord(ev_t0_, compute_));
+  const bool single = tiles_.size() == 1 && !has_exchange_;
+  if (single && opt_.small_grid_lds && !opt_.naive && lds_solver_fits(dec_.NX, dec_.NY) && steps > 0) {
+    // Whole run inside one workgroup's LDS.
+    st.path = "lds";
+    Tile& T = tiles_[0];
+    const int interval = opt_.convergence ? (int)opt_.interval : 0;
+    // The LDS kernel counts steps from 1; align the convergence cadence with steps_done_.
+    if (interval > 0 && steps_done_ % interval != 0)
+      throw std::runtime_error("LDS solver: resume point must be a multiple of the convergence interval");
+    launch_lds_solver(T.buf[T.cur] + T.g.idx(0, 0), T.g.pitch, T.buf[1 - T.cur] + T.g.idx(0, 0), T.g.pitch, T.g.xcell,
+                      T.g.ycell, steps, opt_.precision, opt_.boundary, opt_.cx, opt_.cy, opt_.periodic_x,
+                      opt_.periodic_y, interval, opt_.sensitivity, d_lds_steps_, d_resid_, compute_);
+    H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
+    long long done = 0;
+    H2D_HIP_CHECK(hipMemcpyAsync(&done, d_lds_steps_, sizeof(long long), hipMemcpyDeviceToHost, compute_));
+    H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, sizeof(double), hipMemcpyDeviceToHost, compute_));
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    T.cur = 1 - T.cur;
+    st.converged = done < steps;
+    st.residual = h_resid_[0];
+    steps_done_ += done;
+    st.chunks = 1;
+  } else {
+    st.path = opt_.naive ? "naive" : "stream";
+    while (steps_done_ < target) {
+      bool check = false;
+      const int k = next_chunk(steps_done_, target, &check);
+      if (has_exchange_) {
+        H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
+        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+        do_exchange_async(k);
+        H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
+        ++st.exchanges;
+        if (opt_.overlap && !opt_.naive) {
+          for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1);
+          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+          for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2);
+          for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
+        } else {
+          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+          advance(k, check);
+        }
+      } else {
+        advance(k, check);
+      }
+      ++st.chunks;
+      if (check) {
+        st.residual = finish_residual();
+        if (st.residual < opt_.sensitivity) {
+          rollback();
+          st.converged = true;
+          break;
+        }
+      }
+      steps_done_ += k;
+    }
+    H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
+  }
+  H2D_HIP_CHECK(hipEventSynchronize(ev_t1_));
+  float ms = 0.0f;
+  H2D_HIP_CHECK(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
+  st.device_ms = ms;
+  st.steps_done = steps_done_;
+  st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+  return st;
+}
+
+int64_t Engine::send_count(int t, int k) const {
+  check_tile(t);
+  return make_plan(dec_, tiles_[t].rank, tiles_[t].g, k).send_total;
+}
+
+int64_t Engine::recv_count(int t, int k) const {
+  check_tile(t);
+  return make_plan(dec_, tiles_[t].rank, tiles_[t].g, k).recv_total;
+}
+
+std::vector<int64_t> Engine::plan_info(int t, int k) const {
+  check_tile(t);
+  ExchangePlan p = make_plan(dec_, tiles_[t].rank, tiles_[t].g, k);
+  std::vector<int64_t> v;
+  for (int d = 0; d < kNumDirs; ++d) {
+    v.push_back(p.peer[d]);
+    v.push_back(p.send_off[d]);
+    v.push_back(p.send_rect[d].count());
+    v.push_back(p.recv_off[d]);
+    v.push_back(p.recv_rect[d].count());
+  }
+  return v;
+}
+
+void Engine::pack(int t, int k, uintptr_t sendbuf) {
+  check_tile(t);
+  Tile& T = tiles_[t];
+  ExchangePlan p = make_plan(dec_, T.rank, T.g, k);
+  std::vector<CopyDesc> v;
+  plan_pack_descs(p, T.g, T.buf[T.cur], reinterpret_cast<float*>(sendbuf), v);
+  if (on_gpu()) {
+    if (v.empty()) return;
+    int64_t me = 0;
+    for (auto& c : v) me = std::max(me, c.rows * c.cols);
+    CopyDesc* d = dmalloc<CopyDesc>(v.size());
+    H2D_HIP_CHECK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(CopyDesc), hipMemcpyHostToDevice, compute_));
+    launch_copy_rects(d, (int)v.size(), me, compute_);
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    hipFree(d);
+  } else {
+    cpu_copy_rects(v);
+  }
+}
+
+void Engine::unpack(int t, int k, uintptr_t recvbuf) {
+  check_tile(t);
+  Tile& T = tiles_[t];
+  ExchangePlan p = make_plan(dec_, T.rank, T.g, k);
+  std::vector<CopyDesc> v;
+  plan_unpack_descs(p, T.g, T.buf[T.cur], reinterpret_cast<const float*>(recvbuf), v);
+  if (on_gpu()) {
+    if (v.empty()) return;
+    int64_t me = 0;
+    for (auto& c : v) me = std::max(me, c.rows * c.cols);
+    CopyDesc* d = dmalloc<CopyDesc>(v.size());
+    H2D_HIP_CHECK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(CopyDesc), hipMemcpyHostToDevice, compute_));
+    launch_copy_rects(d, (int)v.size(), me, compute_);
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    hipFree(d);
+  } else {
+    cpu_copy_rects(v);
+  }
+}
+
+std::vector<float> Engine::download(int t) const {
+  check_tile(t);
+  const Tile& T = tiles_[t];
+  std::vector<float> out((size_t)(T.g.xcell * T.g.ycell));
+  if (on_gpu()) {
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    H2D_HIP_CHECK(hipMemcpy2D(out.data(), T.g.ycell * sizeof(float), T.buf[T.cur] + T.g.idx(0, 0),
+                              T.g.pitch * sizeof(float), T.g.ycell * sizeof(float), T.g.xcell, hipMemcpyDeviceToHost));
+  } else {
+    for (int64_t i = 0; i < T.g.xcell; ++i)
+      std::memcpy(&out[(size_t)(i * T.g.ycell)], T.buf[T.cur] + T.g.idx(i, 0), T.g.ycell * sizeof(float));
+  }
+  return out;
+}
+
+void Engine::upload(int t, const float* owned) {
+  check_tile(t);
+  Tile& T = tiles_[t];
+  if (on_gpu()) {
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    H2D_HIP_CHECK(hipMemcpy2D(T.buf[T.cur] + T.g.idx(0, 0), T.g.pitch * sizeof(float), owned, T.g.ycell * sizeof(float),
+                              T.g.ycell * sizeof(float), T.g.xcell, hipMemcpyHostToDevice));
+  } else {
+    for (int64_t i = 0; i < T.g.xcell; ++i)
+      std::memcpy(T.buf[T.cur] + T.g.idx(i, 0), owned + i * T.g.ycell, T.g.ycell * sizeof(float));
+  }
+}
+
+void Engine::synchronize() const {
+  if (on_gpu()) {
+    H2D_HIP_CHECK(hipStreamSynchronize(comm_));
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+  }
+}
+
+std::string Engine::rccl_unique_id() {
+  ncclUniqueId id;
+  H2D_NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+void Engine::init_rccl(const std::string& id, int nranks, int rank) {
+  if (!on_gpu()) throw std::runtime_error("init_rccl needs a GPU engine");
+  if (id.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("bad RCCL unique id");
+  if (nranks != dec_.nranks()) throw std::invalid_argument("RCCL world size must equal gridx*gridy");
+  if (tiles_.size() != 1 || tiles_[0].rank != rank) throw std::invalid_argument("RCCL rank must own exactly its tile");
+  ncclUniqueId uid;
+  std::memcpy(&uid, id.data(), sizeof(uid));
+  H2D_HIP_CHECK(hipSetDevice(opt_.device));
+  ncclComm_t comm;
+  H2D_NCCL_CHECK(ncclCommInitRank(&comm, nranks, uid, rank));
+  rccl_comm_ = comm;
+  rccl_rank_ = rank;
+  rccl_nranks_ = nranks;
+  transport_ = kTransportRccl;
+}
+
+}  // namespace h2d

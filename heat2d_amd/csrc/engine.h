@@ -1,0 +1,169 @@
+// heat2d_amd — the native solver engine (one per process).
+//
+// Replaces the reference's hand-rolled time loops (grad1612_mpi_heat.c:206-280,
+// grad1612_hybrid_heat.c:241-306, grad1612_cuda_heat.cu:79-89, mpi_heat2Dn.c:175-196) with
+// one MI355X-first runtime:
+//   * each process owns one or more halo-padded tiles of a 2-D block decomposition;
+//   * time advances in chunks of K fused steps (temporal blocking) — halos are K deep and
+//     exchanged once per chunk (8-neighbour, corners included) instead of every step;
+//   * per chunk: the halo exchange runs on a dedicated comm stream while the interior work
+//     units (those whose K-cone does not touch the ghost ring) run on the compute stream;
+//     the boundary units wait on the exchange event (the reference's grey/green/yellow
+//     overlap, Report.pdf p.17-18, grad1612_mpi_heat.c:231-275);
+//   * transports: in-process tile-to-tile copies (LocalMultiTile — several logical ranks on
+//     one GPU or on the CPU), RCCL send/recv over xGMI (one process per GPU), or "external"
+//     (the Python layer drives pack/exchange/unpack, e.g. torch.distributed gloo on CPU);
+//   * convergence: Σ(Δ)² fused into the last time level of the chunk that ends on a check
+//     step, deterministic per-wave partials, RCCL all-reduce across ranks (B-5 fixed cadence).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "cpu_reference.h"
+#include "decomposition.h"
+#include "kernels.h"
+
+namespace h2d {
+
+enum Transport : int {
+  kTransportAuto = 0,      // local copies if this process owns every tile, else RCCL
+  kTransportLocal = 1,     // all tiles in this process
+  kTransportRccl = 2,      // one tile per process, RCCL p2p
+  kTransportExternal = 3,  // caller drives pack / unpack
+};
+
+struct EngineOptions {
+  int64_t nx = 10, ny = 10;
+  int gridx = 1, gridy = 1;
+  bool periodic_x = false, periodic_y = false;
+  int boundary = kFixed;
+  int precision = kRef;
+  int init = kInitExact;
+  double cx = kCxDouble, cy = kCxDouble;
+  int tblock = 8;          // max fused steps per chunk (= halo depth)
+  int rows_per_wave = 0;   // H; 0 = automatic
+  bool convergence = false;
+  int64_t interval = 20;
+  double sensitivity = 0.1;
+  int device = 0;          // HIP device ordinal, -1 = CPU
+  std::vector<int> ranks;  // tiles owned by this process (empty = all)
+  int transport = kTransportAuto;
+  bool overlap = true;     // overlap halo exchange with interior compute
+  bool small_grid_lds = true;  // whole-grid LDS solver for small single-tile problems
+  bool naive = false;      // validation: one-thread-per-cell single-step kernel
+};
+
+struct RunStats {
+  int64_t steps_done = 0;
+  bool converged = false;
+  double residual = -1.0;
+  double device_ms = 0.0;  // hipEvent time of the step loop (CPU: wall time)
+  double wall_ms = 0.0;
+  int64_t chunks = 0;
+  int64_t exchanges = 0;
+  std::string path;        // "stream", "lds", "naive", "cpu"
+};
+
+class Engine {
+ public:
+  explicit Engine(const EngineOptions& o);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  const EngineOptions& options() const { return opt_; }
+  const Decomposition& decomposition() const { return dec_; }
+  int num_tiles() const { return (int)tiles_.size(); }
+  int tile_rank(int t) const { return tiles_.at(t).rank; }
+  TileGeom geom(int t) const { return tiles_.at(t).g; }
+  int halo_depth() const { return G_; }
+  bool on_gpu() const { return opt_.device >= 0; }
+  bool has_exchange() const { return has_exchange_; }
+  int rows_per_wave(int K) const;
+  int64_t steps_done() const { return steps_done_; }
+  uintptr_t stream_handle() const { return (uintptr_t)compute_; }
+
+  // RCCL bootstrap: rank 0 creates the id, the caller broadcasts it (torch.distributed).
+  static std::string rccl_unique_id();
+  void init_rccl(const std::string& id, int nranks, int rank);
+  bool rccl_ready() const { return rccl_comm_ != nullptr; }
+
+  // Native time loop (transports local / rccl / none).
+  RunStats run(int64_t steps);
+
+  // Fine-grained API (external transports, tests).
+  int next_chunk(int64_t done, int64_t total, bool* check) const;
+  void advance(int k, bool residual);      // one chunk, all tiles, no exchange
+  void exchange_local(int k);              // in-process halo fill for depth k
+  double local_residual();                 // Σ over local tiles of the last advance(k, true)
+  int64_t send_count(int t, int k) const;
+  int64_t recv_count(int t, int k) const;
+  std::vector<int64_t> plan_info(int t, int k) const;  // [peer, send_off, send_n, recv_off, recv_n] × 8
+  void pack(int t, int k, uintptr_t sendbuf);
+  void unpack(int t, int k, uintptr_t recvbuf);
+  void rollback();  // undo the last chunk (convergence exit)
+  void set_steps_done(int64_t s) { steps_done_ = s; }
+
+  std::vector<float> download(int t) const;  // owned block, row-major xcell×ycell
+  void upload(int t, const float* owned);
+  void synchronize() const;
+
+ private:
+  struct Tile {
+    int rank = 0;
+    TileGeom g;
+    float* buf[2] = {nullptr, nullptr};  // device or host storage
+    std::vector<float> host[2];          // CPU storage
+    std::vector<float> scratch[2];       // CPU temporal-block scratch
+    int cur = 0;
+    double last_resid = 0.0;
+    double* partials = nullptr;  // per-wave residual partials (device)
+    int64_t pcap = 0;
+  };
+  struct UnitLists {
+    int H = 0;
+    Unit* d_all = nullptr;
+    Unit* d_interior = nullptr;
+    Unit* d_boundary = nullptr;
+    int n_all = 0, n_interior = 0, n_boundary = 0;
+  };
+
+  const UnitLists& units(int t, int K);
+  void launch_chunk_tile(int t, int K, bool residual, int which);  // which: 0 all, 1 interior, 2 boundary
+  void do_exchange_async(int K);  // enqueue on comm stream
+  double finish_residual();       // reduce + (rccl) all-reduce, host sync
+  CopyDesc* local_descs(int K, int& n, int64_t& maxe);
+  void check_tile(int t) const;
+
+  EngineOptions opt_;
+  Decomposition dec_;
+  int G_ = 1;
+  bool has_exchange_ = false;
+  int transport_ = kTransportLocal;
+  std::vector<Tile> tiles_;
+  int64_t steps_done_ = 0;
+
+  // device state
+  hipStream_t compute_ = nullptr, comm_ = nullptr;
+  hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_t0_ = nullptr, ev_t1_ = nullptr;
+  std::map<std::pair<int, int>, UnitLists> units_;
+  std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> local_descs_;  // (K, parity)
+  std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> pack_descs_;   // (K, parity) for rccl
+  std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> unpack_descs_;
+  double* d_resid_ = nullptr;       // [num_tiles] + 1 total
+  double* h_resid_ = nullptr;       // pinned
+  long long* d_lds_steps_ = nullptr;
+  float* d_send_ = nullptr;
+  float* d_recv_ = nullptr;
+  int64_t stage_cap_ = 0;
+  void* rccl_comm_ = nullptr;       // ncclComm_t
+  int rccl_rank_ = 0, rccl_nranks_ = 1;
+};
+
+}  // namespace h2d

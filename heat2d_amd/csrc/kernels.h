@@ -1,0 +1,74 @@
+// heat2d_amd — HIP kernel launch interface (gfx950 / CDNA4).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+#include "h2d_common.h"
+
+#define H2D_HIP_CHECK(call)                                                                          \
+  do {                                                                                               \
+    hipError_t _e = (call);                                                                          \
+    if (_e != hipSuccess) {                                                                          \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + __FILE__ + \
+                               ":" + std::to_string(__LINE__) + ": " #call);                        \
+    }                                                                                                \
+  } while (0)
+
+namespace h2d {
+
+// Work unit of the streaming kernel: (strip index, row-segment index).
+struct Unit {
+  int strip;
+  int seg;
+};
+
+// Arguments of the temporally-blocked streaming stencil.
+struct StreamArgs {
+  const float* src;
+  float* dst;
+  const Unit* units;
+  int nunits;
+  int H;       // output rows per unit
+  int wout;    // output columns per strip (256 - 2R)
+  int R;       // column lead (round_up(K,4))
+  int64_t pitch, G, PL;
+  int64_t xcell, ycell;
+  int64_t gx0, gy0, NX, NY;
+  double cx, cy;
+  int fixed;
+  int per_x, per_y;
+  double* partials;  // per-unit residual partial sums (only read by the RESID variant)
+};
+
+// Largest K with a compiled streaming kernel.
+constexpr int kMaxK = 16;
+bool stream_k_supported(int K);
+
+void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hipStream_t s);
+void launch_naive_step(const TileGeom& g, const float* src, float* dst, int precision, int boundary, double cx,
+                       double cy, bool per_x, bool per_y, hipStream_t s);
+void launch_init(const TileGeom& g, float* base, int init, hipStream_t s);
+void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s);
+void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s);
+// Residual of a whole tile (Σ (a-b)² over owned cells) — used by tests/ops.
+void launch_tile_residual(const TileGeom& g, const float* a, const float* b, double* partials, int npartials,
+                          hipStream_t s);
+
+// Small-grid resident solver: the whole grid lives in one workgroup's LDS for all steps.
+bool lds_solver_fits(int64_t NX, int64_t NY);
+void launch_lds_solver(const float* in, int64_t in_pitch, float* out, int64_t out_pitch, int64_t NX, int64_t NY,
+                       int64_t steps, int precision,
+                       int boundary, double cx, double cy, bool per_x, bool per_y, int conv_interval,
+                       double sensitivity, long long* steps_done, double* residual, hipStream_t s);
+
+}  // namespace h2d
+
+namespace h2d {
+template <int K>
+void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s);
+}  // namespace h2d

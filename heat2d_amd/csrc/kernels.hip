@@ -1,0 +1,255 @@
+// heat2d_amd — auxiliary HIP kernels (init, halo copies, reductions, naive step, the
+// small-grid LDS-resident solver) and the streaming-kernel dispatch.  The streaming stencil
+// itself lives in stream_kernel.hpp, instantiated once per K in stream_k*.hip.
+// Compiled with -ffp-contract=off.
+#include "stream_kernel.hpp"
+
+#include <algorithm>
+#include <vector>
+
+namespace h2d {
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// Simple one-thread-per-cell step (validation baseline; same semantics, no temporal blocking).
+// ------------------------------------------------------------------------------------------
+template <bool F32>
+__global__ __launch_bounds__(256) void naive_step_kernel(TileGeom g, const float* __restrict__ src,
+                                                          float* __restrict__ dst, Coef k, int fixed, int per_x,
+                                                          int per_y) {
+  const int64_t j = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int64_t i = (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= g.xcell || j >= g.ycell) return;
+  const int m = max(dim_mode(g.gx0 + i, g.NX, per_x != 0, fixed != 0), dim_mode(g.gy0 + j, g.NY, per_y != 0, fixed != 0));
+  const int64_t c = g.idx(i, j);
+  float v;
+  if (m == 2) v = 0.0f;
+  else if (m == 1) v = src[c];
+  else v = cell<F32>(src[c], src[c - g.pitch], src[c + g.pitch], src[c - 1], src[c + 1], k);
+  dst[c] = v;
+}
+
+__global__ void init_kernel(TileGeom g, float* __restrict__ base, int init) {
+  const int64_t total = g.elems();
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / g.pitch - g.G;
+    const int64_t j = e % g.pitch - g.PL;
+    float v = 0.0f;
+    if (i >= 0 && i < g.xcell && j >= 0 && j < g.ycell) v = init_value(init, g.gx0 + i, g.gy0 + j, g.NX, g.NY);
+    base[e] = v;
+  }
+}
+
+__global__ void copy_rects_kernel(const CopyDesc* __restrict__ descs) {
+  const CopyDesc d = descs[blockIdx.y];
+  const int64_t total = d.rows * d.cols;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / d.cols, cc = e - r * d.cols;
+    d.dst[r * d.dst_pitch + cc] = d.src[r * d.src_pitch + cc];
+  }
+}
+
+// Deterministic single-block sum (fixed summation order).
+__global__ __launch_bounds__(256) void reduce_sum_kernel(const double* __restrict__ in, int n, double* __restrict__ out) {
+  __shared__ double part[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += in[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = ((part[0] + part[1]) + part[2]) + part[3];
+}
+
+__global__ __launch_bounds__(256) void tile_residual_kernel(TileGeom g, const float* __restrict__ a,
+                                                             const float* __restrict__ b, double* __restrict__ partials) {
+  __shared__ double part[4];
+  const int64_t total = g.xcell * g.ycell;
+  double s = 0.0;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / g.ycell, j = e % g.ycell;
+    s += sq_diff(a[g.idx(i, j)], b[g.idx(i, j)]);
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = ((part[0] + part[1]) + part[2]) + part[3];
+}
+
+// ------------------------------------------------------------------------------------------
+// Small-grid resident solver: one 1024-thread workgroup keeps the whole grid in LDS and runs
+// every time step (and the convergence test) without returning to the host.  Replaces
+// ~2 launches/step of the reference CUDA program (grad1612_cuda_heat.cu:82-85) for grids up
+// to 40960 cells, where a GPU is otherwise launch-latency bound.
+// ------------------------------------------------------------------------------------------
+constexpr int kLdsCells = 20480;  // 80 KiB of fp32: 160x128 (the largest grid the reference CUDA table runs in 71 us/step)
+constexpr int kLdsThreads = 1024;
+constexpr int kLdsPerThread = kLdsCells / kLdsThreads;
+
+template <bool F32>
+__global__ __launch_bounds__(1024) void lds_solver_kernel(const float* __restrict__ in, int64_t in_pitch,
+                                                           float* __restrict__ out, int64_t out_pitch, int NX, int NY,
+                                                           long long steps, Coef k, int fixed, int per_x, int per_y,
+                                                           int interval, double sens, long long* steps_done,
+                                                           double* residual) {
+  __shared__ float u[kLdsCells];
+  __shared__ double red[16];
+  __shared__ int stop_flag;
+  const int tid = threadIdx.x;
+  const int ncell = NX * NY;
+  for (int e = tid; e < ncell; e += kLdsThreads) u[e] = in[(int64_t)(e / NY) * in_pitch + (e % NY)];
+  const int di = kLdsThreads / NY, dj = kLdsThreads % NY;
+  const int i0 = tid / NY, j0 = tid % NY;
+  double last_res = -1.0;
+  long long done = 0;
+  __syncthreads();
+  for (long long step = 1; step <= steps; ++step) {
+    float nv[kLdsPerThread];
+    double racc = 0.0;
+    int i = i0, j = j0;
+#pragma unroll
+    for (int q = 0; q < kLdsPerThread; ++q) {
+      const int idx = tid + q * kLdsThreads;
+      if (idx < ncell) {
+        const int m = max(dim_mode(i, NX, per_x != 0, fixed != 0), dim_mode(j, NY, per_y != 0, fixed != 0));
+        const float cc = u[idx];
+        float v;
+        if (m == 2) {
+          v = 0.0f;
+        } else if (m == 1) {
+          v = cc;
+        } else {
+          const float nn = i > 0 ? u[idx - NY] : (per_x ? u[idx + (NX - 1) * NY] : 0.0f);
+          const float ss = i < NX - 1 ? u[idx + NY] : (per_x ? u[idx - (NX - 1) * NY] : 0.0f);
+          const float ww = j > 0 ? u[idx - 1] : (per_y ? u[idx + NY - 1] : 0.0f);
+          const float ee = j < NY - 1 ? u[idx + 1] : (per_y ? u[idx - (NY - 1)] : 0.0f);
+          v = cell<F32>(cc, nn, ss, ww, ee, k);
+        }
+        nv[q] = v;
+        racc += sq_diff(v, cc);
+      }
+      j += dj;
+      i += di;
+      if (j >= NY) {
+        j -= NY;
+        i += 1;
+      }
+    }
+    const bool check = interval > 0 && (step % interval) == 0;
+    if (check) {  // block-uniform
+      racc = wave_sum(racc);
+      if ((tid & 63) == 0) red[tid >> 6] = racc;
+      __syncthreads();
+      if (tid == 0) {
+        double s = 0.0;
+        for (int q = 0; q < kLdsThreads / 64; ++q) s += red[q];
+        red[0] = s;
+        stop_flag = s < sens;
+      }
+      __syncthreads();
+      last_res = red[0];
+      if (stop_flag) break;  // keep the pre-update grid: steps committed = step-1
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kLdsPerThread; ++q) {
+      const int idx = tid + q * kLdsThreads;
+      if (idx < ncell) u[idx] = nv[q];
+    }
+    __syncthreads();
+    done = step;
+  }
+  for (int e = tid; e < ncell; e += kLdsThreads) out[(int64_t)(e / NY) * out_pitch + (e % NY)] = u[e];
+  if (tid == 0) {
+    *steps_done = done;
+    *residual = last_res;
+  }
+}
+
+}  // namespace
+
+#define H2D_K_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(12) X(16)
+#define H2D_EXTERN(K) extern template void launch_stream_k<K>(const StreamArgs&, bool, bool, hipStream_t);
+H2D_K_LIST(H2D_EXTERN)
+#undef H2D_EXTERN
+
+bool stream_k_supported(int K) {
+  switch (K) {
+#define H2D_CASE(KK) case KK: return true;
+    H2D_K_LIST(H2D_CASE)
+#undef H2D_CASE
+    default: return false;
+  }
+}
+
+void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hipStream_t s) {
+  if (a.nunits <= 0) return;
+  if (lead_cols(K) != a.R || kWaveCols - 2 * a.R != a.wout) throw std::invalid_argument("launch_stream: R/wout mismatch");
+  const bool f32 = precision == kFp32;
+  switch (K) {
+#define H2D_CASE(KK) case KK: launch_stream_k<KK>(a, f32, residual, s); break;
+    H2D_K_LIST(H2D_CASE)
+#undef H2D_CASE
+    default: throw std::invalid_argument("no streaming kernel compiled for K=" + std::to_string(K));
+  }
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_naive_step(const TileGeom& g, const float* src, float* dst, int precision, int boundary, double cx,
+                       double cy, bool per_x, bool per_y, hipStream_t s) {
+  if (g.xcell <= 0 || g.ycell <= 0) return;
+  dim3 grid((unsigned)((g.ycell + 63) / 64), (unsigned)((g.xcell + 3) / 4));
+  Coef k{cx, cy, (float)cx, (float)cy};
+  const int fixed = boundary == kFixed;
+  if (precision == kFp32)
+    hipLaunchKernelGGL(naive_step_kernel<true>, grid, dim3(256), 0, s, g, src, dst, k, fixed, (int)per_x, (int)per_y);
+  else
+    hipLaunchKernelGGL(naive_step_kernel<false>, grid, dim3(256), 0, s, g, src, dst, k, fixed, (int)per_x, (int)per_y);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_init(const TileGeom& g, float* base, int init, hipStream_t s) {
+  const int64_t total = g.elems();
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 32);
+  hipLaunchKernelGGL(init_kernel, dim3(blocks), dim3(256), 0, s, g, base, init);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s) {
+  if (ndesc <= 0 || max_elems <= 0) return;
+  const unsigned bx = (unsigned)std::min<int64_t>((max_elems + 255) / 256, 1024);
+  hipLaunchKernelGGL(copy_rects_kernel, dim3(bx, (unsigned)ndesc), dim3(256), 0, s, d_descs);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_sum_kernel, dim3(1), dim3(256), 0, s, in, n, out);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_tile_residual(const TileGeom& g, const float* a, const float* b, double* partials, int npartials,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(tile_residual_kernel, dim3(npartials), dim3(256), 0, s, g, a, b, partials);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+bool lds_solver_fits(int64_t NX, int64_t NY) { return NX >= 1 && NY >= 1 && NX * NY <= kLdsCells; }
+
+void launch_lds_solver(const float* in, int64_t in_pitch, float* out, int64_t out_pitch, int64_t NX, int64_t NY,
+                       int64_t steps, int precision, int boundary, double cx, double cy, bool per_x, bool per_y,
+                       int conv_interval, double sensitivity, long long* steps_done, double* residual,
+                       hipStream_t s) {
+  if (!lds_solver_fits(NX, NY)) throw std::invalid_argument("grid too large for the LDS-resident solver");
+  Coef k{cx, cy, (float)cx, (float)cy};
+  const int fixed = boundary == kFixed;
+  if (precision == kFp32)
+    hipLaunchKernelGGL(lds_solver_kernel<true>, dim3(1), dim3(kLdsThreads), 0, s, in, in_pitch, out, out_pitch,
+                       (int)NX, (int)NY, (long long)steps, k, fixed, (int)per_x, (int)per_y, conv_interval,
+                       sensitivity, steps_done, residual);
+  else
+    hipLaunchKernelGGL(lds_solver_kernel<false>, dim3(1), dim3(kLdsThreads), 0, s, in, in_pitch, out, out_pitch,
+                       (int)NX, (int)NY, (long long)steps, k, fixed, (int)per_x, (int)per_y, conv_interval,
+                       sensitivity, steps_done, residual);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace h2d

@@ -1,0 +1,6 @@
+// Instantiation of the streaming stencil for K = 3 fused time steps (see stream_kernel.hpp).
+#include "stream_kernel.hpp"
+
+namespace h2d {
+template void launch_stream_k<3>(const StreamArgs&, bool, bool, hipStream_t);
+}  // namespace h2d

@@ -1,0 +1,107 @@
+"""Process runtime: one process per GPU, bootstrapped with ``torch.distributed``.
+
+Replaces ``MPI_Init / Comm_size / Comm_rank`` (``grad1612_mpi_heat.c:42-44``) and the
+timing collectives ``MPI_Barrier`` + ``MPI_Reduce(MAX)`` (``:206,277-280``).
+
+Planes:
+  * control plane (bootstrap of the RCCL unique id, barriers, elapsed-time max, convergence
+    sums of the external transport): a ``gloo`` process group — host-side, works with or
+    without GPUs and is exercised by the CPU test-suite with world_size > 1;
+  * data plane on GPUs: the engine's own RCCL communicator (ncclSend/ncclRecv over xGMI,
+    ncclAllReduce for the convergence residual), created from a unique id broadcast on the
+    control plane.  ``--transport torch`` instead moves halos with ``torch.distributed``
+    (``nccl`` backend = RCCL on ROCm) batch_isend_irecv.
+
+Rendezvous always uses the env:// variables set by ``torch.distributed.run``
+(``MASTER_ADDR=127.0.0.1`` recommended).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    initialized_here: bool = False
+    nccl_group: Optional[object] = None
+
+    @property
+    def is_multi(self) -> bool:
+        return self.world > 1
+
+    # ---- collectives on the control plane --------------------------------------------------
+    def barrier(self) -> None:
+        if self.is_multi:
+            dist.barrier()
+
+    def allreduce_max(self, x: float) -> float:
+        if not self.is_multi:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allreduce_sum(self, x: float) -> float:
+        if not self.is_multi:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def broadcast_bytes(self, data: Optional[bytes], src: int = 0) -> bytes:
+        if not self.is_multi:
+            assert data is not None
+            return data
+        obj = [data if self.rank == src else None]
+        dist.broadcast_object_list(obj, src=src)
+        return obj[0]
+
+    def gather_objects(self, obj, dst: int = 0):
+        if not self.is_multi:
+            return [obj]
+        out = [None] * self.world if self.rank == dst else None
+        dist.gather_object(obj, out, dst=dst)
+        return out
+
+    def get_nccl_group(self):
+        """Lazily created RCCL-backed group for the torch p2p transport on GPUs."""
+        if self.nccl_group is None:
+            self.nccl_group = dist.new_group(backend="nccl")
+        return self.nccl_group
+
+    def shutdown(self) -> None:
+        if self.initialized_here and dist.is_initialized():
+            dist.destroy_process_group()
+            self.initialized_here = False
+
+
+def env_world() -> tuple[int, int, int]:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def init_distributed(timeout_s: float = 600.0) -> DistContext:
+    """Initialise the control plane from the environment (no-op for a single process)."""
+    rank, world, local = env_world()
+    ctx = DistContext(rank=rank, world=world, local_rank=local)
+    if world > 1:
+        if dist.is_initialized():
+            ctx.rank, ctx.world = dist.get_rank(), dist.get_world_size()
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29500")
+            dist.init_process_group(backend="gloo", init_method="env://", rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s))
+            ctx.initialized_here = True
+    return ctx

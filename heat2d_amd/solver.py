@@ -1,0 +1,223 @@
+"""Solver: the top-level driver (one per process).
+
+Equivalent of the reference programs' ``main()`` (``grad1612_mpi_heat.c:27-315``,
+``mpi_heat2Dn.c:46-222``, ``grad1612_hybrid_heat.c:30-352``, ``grad1612_cuda_heat.cu:64-93``):
+configuration, decomposition, allocation + initial field, initial output, the timed step
+loop, timing reduction, final output.
+
+Execution modes
+  * one process, GPU   : every tile of the GRIDX×GRIDY decomposition lives on the one device
+                         (LocalMultiTile: halos are device-to-device copies) — 1×1 is the
+                         plain single-GPU run of ``grad1612_cuda_heat.cu``;
+  * one process, CPU   : the same engine on host memory (test oracle path);
+  * N processes, GPU   : one tile per rank, native RCCL halo exchange over xGMI (default) or
+                         ``--transport torch`` (torch.distributed p2p);
+  * N processes, CPU   : one tile per rank, torch.distributed (gloo) p2p — the CI path.
+"""
+from __future__ import annotations
+
+import socket
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ._native import gpu_available, native
+from .config import Config
+from .parallel import topology
+from .parallel.dist import DistContext, init_distributed
+from .parallel.exchange import TorchHaloExchanger
+from .utils import io as h2io
+from .utils.device import device_report
+from .utils.report import Reporter, metrics
+
+
+@dataclass
+class RunResult:
+    steps_done: int
+    converged: bool
+    residual: float
+    elapsed_s: float  # max over ranks of the loop's wall time
+    device_ms: float  # this rank's device-event time of the loop
+    path: str
+    chunks: int
+    exchanges: int
+    nranks: int
+    ntiles: int
+    extra: dict = field(default_factory=dict)
+
+
+class Solver:
+    def __init__(self, cfg: Config, ctx: Optional[DistContext] = None, device_ordinal: Optional[int] = None):
+        self.cfg = cfg
+        self.ctx = ctx or init_distributed()
+        self.model = cfg.model()
+        n = native()
+        want_gpu = cfg.device in ("auto", "gpu")
+        self.on_gpu = want_gpu and gpu_available()
+        if cfg.device == "gpu" and not self.on_gpu:
+            raise RuntimeError("--device gpu requested but no HIP device is available")
+        world = self.ctx.world
+        self.gridx, self.gridy = cfg.resolve_grid(world)
+        self.nranks = self.gridx * self.gridy
+        if world > 1 and self.nranks != world:
+            raise SystemExit(f"ERROR: the number of tasks must be equal to {self.nranks}.\nQuiting...")
+        self.dec = topology.decomposition(cfg.nx, cfg.ny, self.gridx, self.gridy, self.model.periodic_x,
+                                          self.model.periodic_y)
+        ranks = list(range(self.nranks)) if world == 1 else [self.ctx.rank]
+
+        if world == 1:
+            transport = n.TRANSPORT_LOCAL
+        elif self.on_gpu and cfg.transport in ("auto", "rccl"):
+            transport = n.TRANSPORT_RCCL
+        else:
+            transport = n.TRANSPORT_EXTERNAL
+        if self.on_gpu:
+            ndev = n.device_count()
+            self.device = device_ordinal if device_ordinal is not None else (self.ctx.local_rank % ndev)
+            torch.cuda.set_device(self.device)
+        else:
+            self.device = -1
+        self.transport = transport
+        self.engine = n.Engine(
+            cfg.nx, cfg.ny, gridx=self.gridx, gridy=self.gridy, periodic_x=self.model.periodic_x,
+            periodic_y=self.model.periodic_y, boundary=self.model.boundary_id(), precision=self.model.precision_id(),
+            init=self.model.init_id(), cx=self.model.cx, cy=self.model.cy, tblock=cfg.tblock,
+            rows_per_wave=cfg.rows_per_wave, convergence=cfg.convergence, interval=cfg.interval,
+            sensitivity=cfg.sensitivity, device=self.device, ranks=ranks, transport=transport,
+            overlap=cfg.overlap, small_grid_lds=cfg.small_grid, naive=cfg.naive)
+        self.exchanger = None
+        if transport == n.TRANSPORT_RCCL and self.engine.has_exchange():
+            uid = n.Engine.rccl_unique_id() if self.ctx.rank == 0 else None
+            uid = self.ctx.broadcast_bytes(uid)
+            self.engine.init_rccl(uid, world, self.ctx.rank)
+        elif transport == n.TRANSPORT_EXTERNAL and self.engine.has_exchange():
+            dev = torch.device("cuda", self.device) if self.on_gpu else torch.device("cpu")
+            group = self.ctx.get_nccl_group() if self.on_gpu else None
+            self.exchanger = TorchHaloExchanger(self.engine, 0, dev, group)
+        if cfg.load:
+            full = h2io.read_binary(cfg.load, cfg.nx, cfg.ny)
+            for t in range(self.engine.num_tiles()):
+                g = self.engine.geom(t)
+                self.engine.upload(t, full[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]])
+            self.engine.set_steps_done(cfg.start_step)
+        self.reporter = Reporter(cfg.report, enabled=(self.ctx.rank == 0 and not cfg.quiet))
+
+    # ---- data access -------------------------------------------------------------------
+    def tiles(self):
+        """Yield (gx0, gy0, owned block) for every tile held by this process."""
+        for t in range(self.engine.num_tiles()):
+            g = self.engine.geom(t)
+            yield g["gx0"], g["gy0"], self.engine.download(t)
+
+    def gather(self) -> Optional[np.ndarray]:
+        """Full NX×NY grid on rank 0 (None elsewhere).  For tests and small grids."""
+        parts = self.ctx.gather_objects(list(self.tiles()))
+        if self.ctx.rank != 0:
+            return None
+        out = np.zeros((self.cfg.nx, self.cfg.ny), dtype=np.float32)
+        for plist in parts:
+            for gx0, gy0, b in plist:
+                out[gx0:gx0 + b.shape[0], gy0:gy0 + b.shape[1]] = b
+        return out
+
+    def write(self, which: str) -> None:
+        c = self.cfg
+        binary = c.output in ("binary", "both")
+        text = c.output in ("text", "both")
+        h2io.write_grid(c.outdir, which, c.nx, c.ny, self.tiles, rank=self.ctx.rank, barrier=self.ctx.barrier,
+                        binary=binary, text=text, text_style=c.text_style)
+
+    # ---- the run ----------------------------------------------------------------------
+    def _python_loop(self, steps: int) -> dict:
+        """Chunk loop for the external (torch.distributed) transport."""
+        eng, c = self.engine, self.cfg
+        start = eng.steps_done()
+        total = start + steps
+        done = start
+        st = {"converged": False, "residual": -1.0, "chunks": 0, "exchanges": 0}
+        while done < total:
+            k, check = eng.next_chunk(done, total)
+            if self.exchanger is not None:
+                self.exchanger.exchange(k)
+                st["exchanges"] += 1
+            eng.advance(k, check)
+            st["chunks"] += 1
+            if check:
+                r = self.ctx.allreduce_sum(eng.local_residual())
+                st["residual"] = r
+                if r < c.sensitivity:
+                    eng.rollback()
+                    st["converged"] = True
+                    break
+            done += k
+        eng.set_steps_done(done)
+        eng.synchronize()
+        st["steps_done"] = done
+        st["device_ms"] = 0.0
+        st["path"] = "external"
+        return st
+
+    def run(self, steps: Optional[int] = None) -> RunResult:
+        steps = self.cfg.steps if steps is None else steps
+        self.ctx.barrier()
+        self.engine.synchronize()
+        t0 = time.perf_counter()
+        if self.transport == native().TRANSPORT_EXTERNAL and self.engine.has_exchange():
+            st = self._python_loop(steps)
+        else:
+            st = self.engine.run(steps)
+        self.engine.synchronize()
+        local = time.perf_counter() - t0
+        elapsed = self.ctx.allreduce_max(local)
+        return RunResult(steps_done=int(st["steps_done"]), converged=bool(st["converged"]),
+                         residual=float(st["residual"]), elapsed_s=elapsed, device_ms=float(st["device_ms"]),
+                         path=str(st["path"]), chunks=int(st["chunks"]), exchanges=int(st["exchanges"]),
+                         nranks=self.nranks, ntiles=self.engine.num_tiles())
+
+    def main(self) -> RunResult:
+        """Full program: banners, initial output, timed loop, final output, metrics."""
+        c, rep = self.cfg, self.reporter
+        g0 = self.dec.tile(0, 0)
+        strips = topology.strips_table(self.dec) if c.report == "heat2dn" else None
+        if c.debug and self.ctx.rank == 0 and self.on_gpu:
+            rep._p(device_report())
+        rep.start(nprocs=self.nranks, nx=c.nx, ny=c.ny, xcell=g0["xcell"], ycell=g0["ycell"], steps=c.steps,
+                  convergence=c.convergence, interval=c.interval, numthreads=c.numthreads, strips=strips)
+        if c.debug:
+            host = socket.gethostname()
+            for t in range(self.engine.num_tiles()):
+                r = self.engine.tile_rank(t)
+                Reporter(c.report, enabled=not c.quiet).debug_neighbors(r, topology.neighbors(self.dec, r), host)
+        if c.output != "none":
+            rep.writing_initial()
+            self.write("initial")
+        rep.begin_steps(strips)
+        res = self.run()
+        rep.finish(steps_done=res.steps_done, elapsed_s=res.elapsed_s, writes_final=c.output != "none")
+        if c.output != "none":
+            self.write("final")
+        if c.save:
+            self.save(c.save)
+        if c.json and self.ctx.rank == 0:
+            rep.json_line(metrics(c.nx, c.ny, res.steps_done, res.elapsed_s, ranks=self.nranks,
+                                  tiles=res.ntiles, path=res.path, converged=res.converged,
+                                  residual=res.residual, device="gpu" if self.on_gpu else "cpu",
+                                  precision=c.precision, boundary=c.boundary, tblock=self.engine.halo_depth(),
+                                  chunks=res.chunks, exchanges=res.exchanges))
+        return res
+
+    def save(self, path: str) -> None:
+        """Checkpoint: the raw NX×NY grid (same layout as final_binary.dat)."""
+        n = native()
+        if self.ctx.rank == 0:
+            n.binary_create(path, self.cfg.nx, self.cfg.ny)
+        self.ctx.barrier()
+        for gx0, gy0, b in self.tiles():
+            n.binary_write_tile(path, self.cfg.nx, self.cfg.ny, gx0, gy0, b)
+        self.ctx.barrier()
+
+    def close(self) -> None:
+        self.engine = None
