@@ -1,0 +1,125 @@
+"""Headline benchmark: cell-updates/s of the 5-point Jacobi heat stencil on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched
+by ``torch.distributed.run`` with one rank per GPU.  A "step" is one Jacobi time step of the
+whole grid.  W untimed warm-up steps, then EXACTLY K timed steps bracketed by a barrier and
+``torch.cuda.synchronize()`` on both sides; the max over ranks is reported by rank 0 as one
+JSON line.
+
+Config (BASELINE.json): 4096×4096 fp32 grid, 1000 steps, center-hot initial field
+(synthetic — computed on device from the exact fp64 formula; no dataset involved).
+Numerics: the bit-exact reference expression (fp32 storage, fp64 arithmetic exactly as the
+reference's C evaluates it) unless ``--precision fp32``.
+
+Scaling: ``--scaling weak`` (default) gives every GPU a 4096×4096 tile (global grid
+4096·GRIDX × 4096·GRIDY, 2-D block decomposition, RCCL halo exchange over xGMI overlapped
+with interior compute); ``--scaling strong`` splits one 4096×4096 grid over the N GPUs.
+``vs_baseline`` divides by the reference's best published throughput, 1.01e10 cell-updates/s
+(2560×2048, 160 MPI tasks on 20 nodes, Report.pdf p.21 Table 1 — BASELINE.md).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_CUPS = 1.01e10
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--n", type=int, default=4096, help="grid side (per GPU for weak scaling)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--precision", choices=("ref", "fp32"), default="ref")
+    ap.add_argument("--boundary", choices=("fixed", "ghost-zero"), default="fixed")
+    ap.add_argument("--tblock", type=int, default=8)
+    ap.add_argument("--rows-per-wave", type=int, default=0)
+    ap.add_argument("--transport", choices=("auto", "rccl", "torch"), default="auto")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--repeat", type=int, default=1, help="timed repetitions (best reported)")
+    a = ap.parse_args()
+
+    import torch
+
+    from heat2d_amd.config import Config, auto_grid
+    from heat2d_amd.parallel.dist import init_distributed
+    from heat2d_amd.solver import Solver
+
+    ctx = init_distributed()
+    world = ctx.world
+    if world != a.gpus and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    gx, gy = auto_grid(world)
+    if a.scaling == "weak":
+        nx, ny = a.n * gx, a.n * gy
+    else:
+        nx = ny = a.n
+    cfg = Config(preset="heat2d", nx=nx, ny=ny, steps=a.steps, gridx=gx, gridy=gy, boundary=a.boundary,
+                 precision=a.precision, init="exact", output="none", device="gpu", transport=a.transport,
+                 tblock=a.tblock, rows_per_wave=a.rows_per_wave, overlap=not a.no_overlap, quiet=True,
+                 report="grad", text_style="grad")
+    s = Solver(cfg, ctx)
+
+    def sync_barrier():
+        torch.cuda.synchronize()
+        ctx.barrier()
+        torch.cuda.synchronize()
+
+    # warm-up (untimed): also builds every lazy structure and warms caches
+    if a.warmup > 0:
+        s.engine.run(a.warmup)
+    best = None
+    res = None
+    for _ in range(max(1, a.repeat)):
+        sync_barrier()
+        t0 = time.perf_counter()
+        res = s.engine.run(a.steps)
+        sync_barrier()
+        dt = ctx.allreduce_max(time.perf_counter() - t0)
+        best = dt if best is None else min(best, dt)
+    if res["steps_done"] - (a.warmup if a.warmup > 0 else 0) < 0:
+        raise SystemExit("bench: step accounting error")
+    cups = float(nx) * float(ny) * a.steps / best
+    if ctx.rank == 0:
+        out = {
+            "metric": "cell-updates/sec (whole node), 4096^2 grid 1000 steps",
+            "value": cups,
+            "unit": "cell-updates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": best * 1e3 / a.steps,
+            "higher_is_better": True,
+            "scaling": a.scaling,
+            "vs_baseline": cups / BASELINE_CUPS,
+            "dtype": "fp32",
+            "compute": ("fp64 expression, bit-exact with the reference" if a.precision == "ref" else "fp32 FMA"),
+            "data": "synthetic center-hot initial field (exact formula, generated on device)",
+            "elapsed_s": best,
+            "config": {
+                "model": "heat2d 5-point Jacobi, fixed edges" if a.boundary == "fixed" else "heat2d 5-point Jacobi, zero ghost ring",
+                "grid": [nx, ny],
+                "grid_per_gpu": [nx // gx, ny // gy],
+                "global_batch": nx * ny,
+                "seq_len": a.steps,
+                "parallelism": f"blocks{gx}x{gy}" if world > 1 else "single",
+                "tblock": s.engine.halo_depth(),
+                "path": res["path"],
+                "transport": cfg.transport,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    ctx.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

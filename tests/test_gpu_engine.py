@@ -1,0 +1,163 @@
+"""GPU tests: the HIP kernels and the native engine against the bit-exact CPU oracle.
+
+Every result in the ``ref`` precision must be bit-identical to ``oracle_run`` (the serial
+reference semantics); fp32 results must be bit-identical to the CPU engine's fp32 path
+(both use fused multiply-adds) and within tolerance of a plain PyTorch fp32 stencil.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(1, 1), (2, 3), (7, 5), (37, 250), (64, 256), (100, 517), (257, 241), (300, 1000)]
+
+
+def oracle(n, nx, ny, steps, boundary=0, precision=0, init=0, per=(False, False), **kw):
+    return n.oracle_run(nx, ny, steps, boundary=boundary, precision=precision, init=init, periodic_x=per[0],
+                        periodic_y=per[1], **kw)
+
+
+@pytest.mark.parametrize("nx,ny", SIZES)
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_stream_single_tile_bitexact(native, gpu, nx, ny, boundary):
+    steps = 23
+    eng = native.Engine(nx, ny, boundary=boundary, tblock=8, device=gpu, small_grid_lds=False)
+    st = eng.run(steps)
+    assert st["path"] == "stream" and st["steps_done"] == steps
+    ref = oracle(native, nx, ny, steps, boundary)["grid"]
+    got = eng.download(0)
+    assert np.array_equal(got, ref), np.abs(got - ref).max()
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16])
+def test_every_compiled_K(native, gpu, K):
+    nx, ny, steps = 203, 611, 2 * K + 3
+    for boundary in (0, 1):
+        eng = native.Engine(nx, ny, boundary=boundary, tblock=K, device=gpu, small_grid_lds=False,
+                            rows_per_wave=max(16, 4 * K))
+        assert eng.halo_depth() == K
+        eng.run(steps)
+        ref = oracle(native, nx, ny, steps, boundary)["grid"]
+        assert np.array_equal(eng.download(0), ref), (K, boundary)
+
+
+@pytest.mark.parametrize("H", [1, 5, 16, 64, 300])
+def test_rows_per_wave_variants(native, gpu, H):
+    nx, ny, steps = 150, 300, 17
+    eng = native.Engine(nx, ny, tblock=8, rows_per_wave=H, device=gpu, small_grid_lds=False)
+    eng.run(steps)
+    assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps)["grid"])
+
+
+def test_int32_init_and_float_coeff(native, gpu):
+    nx, ny, steps = 640, 512, 9
+    cx = native.CX_FLOAT
+    eng = native.Engine(nx, ny, init=native.INIT_INT32, cx=cx, cy=cx, device=gpu, small_grid_lds=False)
+    eng.run(steps)
+    ref = oracle(native, nx, ny, steps, init=1, cx=cx, cy=cx)["grid"]
+    assert np.array_equal(eng.download(0), ref)
+
+
+def test_fp32_matches_cpu_fp32_and_torch(native, gpu):
+    nx, ny, steps = 211, 333, 30
+    g = native.Engine(nx, ny, precision=native.FP32, device=gpu, small_grid_lds=False)
+    g.run(steps)
+    c = native.Engine(nx, ny, precision=native.FP32, device=-1)
+    c.run(steps)
+    got = g.download(0)
+    assert np.array_equal(got, c.download(0))
+    # plain PyTorch fp32 reference of the same op
+    u = torch.from_numpy(native.init_global(nx, ny, 0)).double()
+    for _ in range(steps):
+        v = u.clone()
+        v[1:-1, 1:-1] = u[1:-1, 1:-1] + 0.1 * (u[2:, 1:-1] + u[:-2, 1:-1] - 2 * u[1:-1, 1:-1]) + \
+            0.1 * (u[1:-1, 2:] + u[1:-1, :-2] - 2 * u[1:-1, 1:-1])
+        u = v.float().double()
+    ref = u.float().numpy()
+    rel = np.abs(got - ref).max() / np.abs(ref).max()
+    assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("nx,ny", [(10, 10), (80, 64), (160, 128), (33, 7)])
+def test_lds_small_grid_solver(native, gpu, nx, ny):
+    steps = 1000
+    for boundary in (0, 1):
+        eng = native.Engine(nx, ny, boundary=boundary, device=gpu)
+        st = eng.run(steps)
+        assert st["path"] == "lds"
+        assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, boundary)["grid"])
+
+
+def test_naive_kernel(native, gpu):
+    nx, ny, steps = 129, 257, 11
+    eng = native.Engine(nx, ny, boundary=1, device=gpu, naive=True)
+    st = eng.run(steps)
+    assert st["path"] == "naive"
+    assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, 1)["grid"])
+
+
+@pytest.mark.parametrize("gx,gy", [(1, 2), (2, 1), (2, 2), (2, 4), (4, 2), (3, 3)])
+@pytest.mark.parametrize("overlap", [True, False])
+def test_local_multitile_decomposition_invariance(native, gpu, gx, gy, overlap):
+    nx, ny, steps = 301, 599, 41
+    for boundary in (0, 1):
+        eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=boundary, tblock=8, device=gpu, overlap=overlap)
+        st = eng.run(steps)
+        assert st["exchanges"] > 0
+        out = np.zeros((nx, ny), np.float32)
+        for t in range(eng.num_tiles()):
+            g = eng.geom(t)
+            out[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]] = eng.download(t)
+        assert np.array_equal(out, oracle(native, nx, ny, steps, boundary)["grid"]), (gx, gy, boundary)
+
+
+def test_periodic_multitile(native, gpu):
+    nx, ny, steps = 120, 260, 30
+    eng = native.Engine(nx, ny, gridx=2, gridy=2, periodic_x=True, periodic_y=True, boundary=1, device=gpu)
+    eng.run(steps)
+    out = np.zeros((nx, ny), np.float32)
+    for t in range(4):
+        g = eng.geom(t)
+        out[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]] = eng.download(t)
+    assert np.array_equal(out, oracle(native, nx, ny, steps, 1, per=(True, True))["grid"])
+
+
+@pytest.mark.parametrize("gx,gy", [(1, 1), (2, 2)])
+def test_convergence_matches_oracle(native, gpu, gx, gy):
+    nx, ny = 40, 40
+    kw = dict(convergence=True, interval=20, sensitivity=0.1)
+    ref = oracle(native, nx, ny, 20000, 0, **kw)
+    assert ref["converged"]
+    for lds in (True, False):
+        eng = native.Engine(nx, ny, gridx=gx, gridy=gy, device=gpu, small_grid_lds=lds, **kw)
+        st = eng.run(20000)
+        assert st["converged"] and st["steps_done"] == ref["steps_done"], (st, ref["steps_done"])
+        out = np.zeros((nx, ny), np.float32)
+        for t in range(eng.num_tiles()):
+            g = eng.geom(t)
+            out[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]] = eng.download(t)
+        assert np.array_equal(out, ref["grid"])
+
+
+def test_rccl_self_exchange_periodic(native, gpu):
+    """One rank, periodic in both dims: every halo goes through ncclSend/ncclRecv to itself."""
+    nx, ny, steps = 96, 300, 25
+    eng = native.Engine(nx, ny, periodic_x=True, periodic_y=True, boundary=1, device=gpu, ranks=[0],
+                        transport=native.TRANSPORT_RCCL)
+    eng.init_rccl(native.Engine.rccl_unique_id(), 1, 0)
+    st = eng.run(steps)
+    assert st["exchanges"] > 0
+    assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, 1, per=(True, True))["grid"])
+
+
+def test_rccl_convergence_allreduce(native, gpu):
+    nx, ny = 48, 40
+    kw = dict(convergence=True, interval=10, sensitivity=1e3)
+    ref = oracle(native, nx, ny, 5000, 1, per=(True, False), **kw)
+    eng = native.Engine(nx, ny, periodic_x=True, boundary=1, device=gpu, ranks=[0], transport=native.TRANSPORT_RCCL,
+                        **kw)
+    eng.init_rccl(native.Engine.rccl_unique_id(), 1, 0)
+    st = eng.run(5000)
+    assert st["steps_done"] == ref["steps_done"] and st["converged"] == ref["converged"]
+    assert np.array_equal(eng.download(0), ref["grid"])
