@@ -102,16 +102,6 @@ py::dict device_props(int dev) {
   return d;
 }
 
-// Build the all-units list of a tile on the host (raw-pointer ops path).
-std::vector<Unit> all_units(const TileGeom& g, int K, int H) {
-  std::vector<Unit> v;
-  const int64_t wout = strip_out_cols(K);
-  const int64_t ns = (g.ycell + wout - 1) / wout, nq = (g.xcell + H - 1) / H;
-  for (int64_t s = 0; s < ns; ++s)
-    for (int64_t q = 0; q < nq; ++q) v.push_back(Unit{(int)s, (int)q});
-  return v;
-}
-
 }  // namespace
 
 PYBIND11_MODULE(_heat2d, m) {
@@ -228,7 +218,7 @@ PYBIND11_MODULE(_heat2d, m) {
       .def(py::init([](int64_t nx, int64_t ny, int gridx, int gridy, bool per_x, bool per_y, int boundary,
                        int precision, int init, double cx, double cy, int tblock, int rows_per_wave, bool convergence,
                        int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
-                       bool overlap, bool small_grid_lds, bool naive) {
+                       bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity) {
              EngineOptions o;
              o.nx = nx;
              o.ny = ny;
@@ -252,6 +242,8 @@ PYBIND11_MODULE(_heat2d, m) {
              o.overlap = overlap;
              o.small_grid_lds = small_grid_lds;
              o.naive = naive;
+             o.edge_weight = edge_weight;
+             o.wave_capacity = wave_capacity;
              return new Engine(o);
            }),
            py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
@@ -260,7 +252,8 @@ PYBIND11_MODULE(_heat2d, m) {
            py::arg("tblock") = 8, py::arg("rows_per_wave") = 0, py::arg("convergence") = false,
            py::arg("interval") = 20, py::arg("sensitivity") = 0.1, py::arg("device") = 0,
            py::arg("ranks") = std::vector<int>{}, py::arg("transport") = (int)kTransportAuto,
-           py::arg("overlap") = true, py::arg("small_grid_lds") = true, py::arg("naive") = false)
+           py::arg("overlap") = true, py::arg("small_grid_lds") = true, py::arg("naive") = false,
+           py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0)
       .def("num_tiles", &Engine::num_tiles)
       .def("tile_rank", &Engine::tile_rank)
       .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })
@@ -268,6 +261,7 @@ PYBIND11_MODULE(_heat2d, m) {
       .def("has_exchange", &Engine::has_exchange)
       .def("on_gpu", &Engine::on_gpu)
       .def("rows_per_wave", &Engine::rows_per_wave)
+      .def("num_units", &Engine::num_units)
       .def("steps_done", &Engine::steps_done)
       .def("set_steps_done", &Engine::set_steps_done)
       .def("stream_handle", &Engine::stream_handle)
@@ -355,7 +349,7 @@ PYBIND11_MODULE(_heat2d, m) {
         if (!stream_k_supported(K)) throw std::invalid_argument("unsupported K");
         if (K > g.G) throw std::invalid_argument("K exceeds the tile's ghost depth");
         if (H <= 0) H = 64;
-        std::vector<Unit> u = all_units(g, K, H);
+        std::vector<Unit> u = build_units(g, K, H, boundary == kFixed, per_x, per_y, 1.0, 1 << 30);
         Unit* du = nullptr;
         hipStream_t s = reinterpret_cast<hipStream_t>(stream);
         H2D_HIP_CHECK(hipMalloc(&du, u.size() * sizeof(Unit)));
@@ -365,7 +359,6 @@ PYBIND11_MODULE(_heat2d, m) {
         a.dst = reinterpret_cast<float*>(dst);
         a.units = du;
         a.nunits = (int)u.size();
-        a.H = H;
         a.R = (int)lead_cols(K);
         a.wout = (int)strip_out_cols(K);
         a.pitch = g.pitch;
@@ -383,9 +376,13 @@ PYBIND11_MODULE(_heat2d, m) {
         a.per_x = per_x;
         a.per_y = per_y;
         a.partials = reinterpret_cast<double*>(partials);
+        float* dummy = nullptr;
+        H2D_HIP_CHECK(hipMalloc(&dummy, 4 * kWaveCols * sizeof(float)));
+        a.dummy = dummy;
         launch_stream(a, K, precision, partials != 0, s);
         H2D_HIP_CHECK(hipStreamSynchronize(s));
         H2D_HIP_CHECK(hipFree(du));
+        H2D_HIP_CHECK(hipFree(dummy));
         return (int)u.size();
       },
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("K"), py::arg("precision") = (int)kRef,
@@ -404,6 +401,7 @@ PYBIND11_MODULE(_heat2d, m) {
       py::arg("periodic_x") = false, py::arg("periodic_y") = false, py::arg("stream") = 0);
   m.def("stream_k_supported", &stream_k_supported);
   m.def("lds_solver_fits", &lds_solver_fits);
+  m.def("stream_wave_capacity", &stream_wave_capacity);
   m.def("lead_cols", &lead_cols);
   m.def("strip_out_cols", &strip_out_cols);
 }

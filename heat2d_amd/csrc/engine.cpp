@@ -71,6 +71,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     d_resid_ = dmalloc<double>(ranks.size() + 1);
     H2D_HIP_CHECK(hipHostMalloc(&h_resid_, sizeof(double) * (ranks.size() + 1)));
     d_lds_steps_ = dmalloc<long long>(1);
+    d_dummy_ = dmalloc<float>(4 * kWaveCols);
   }
 
   for (int r : ranks) {
@@ -128,6 +129,7 @@ Engine::~Engine() {
   hipFree(d_resid_);
   hipHostFree(h_resid_);
   hipFree(d_lds_steps_);
+  hipFree(d_dummy_);
   hipFree(d_send_);
   hipFree(d_recv_);
   hipEventDestroy(ev_ready_);
@@ -143,20 +145,18 @@ void Engine::check_tile(int t) const {
 }
 
 int Engine::rows_per_wave(int K) const {
-  if (opt_.rows_per_wave > 0) return opt_.rows_per_wave;
-  // Enough waves to fill 256 CUs × ~8 waves while keeping the K-row cone overhead
-  // ((K-1)/H) small: H in [16, 256].
-  int64_t waves_wanted = 2048;
-  int64_t total_strips = 0, max_rows = 1;
-  for (const Tile& t : tiles_) {
-    total_strips += (t.g.ycell + strip_out_cols(K) - 1) / strip_out_cols(K);
-    max_rows = std::max(max_rows, t.g.xcell);
+  auto it = units_.find(std::make_pair(0, K));
+  if (it != units_.end()) return it->second.H;
+  return opt_.rows_per_wave;
+}
+
+int Engine::num_units(int K) const {
+  int n = 0;
+  for (int t = 0; t < (int)tiles_.size(); ++t) {
+    auto it = units_.find(std::make_pair(t, K));
+    if (it != units_.end()) n += it->second.n_all;
   }
-  int64_t segs = std::max<int64_t>(1, waves_wanted / std::max<int64_t>(1, total_strips));
-  int64_t H = (max_rows + segs - 1) / segs;
-  H = std::max<int64_t>(H, std::max<int64_t>(16, 4 * K));
-  H = std::min<int64_t>(H, 256);
-  return (int)H;
+  return n;
 }
 
 const Engine::UnitLists& Engine::units(int t, int K) {
@@ -166,28 +166,33 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   const Tile& tl = tiles_[t];
   const TileGeom& g = tl.g;
   UnitLists L;
-  L.H = rows_per_wave(K);
   const int64_t wout = strip_out_cols(K);
-  const int64_t nstrips = (g.ycell + wout - 1) / wout;
-  const int64_t nsegs = (g.xcell + L.H - 1) / L.H;
-  if (nstrips * nsegs > (1LL << 30)) throw std::runtime_error("too many work units");
   std::array<bool, kNumDirs> peer;
   for (int d = 0; d < kNumDirs; ++d) peer[d] = dec_.neighbor(tl.rank, d) >= 0;
-  std::vector<Unit> all, in, bd;
-  for (int64_t s = 0; s < nstrips; ++s) {
-    const int64_t y0 = s * wout, y1 = std::min(g.ycell, y0 + wout);
+  const int64_t cap = opt_.wave_capacity > 0 ? opt_.wave_capacity : stream_wave_capacity(K, opt_.precision, opt_.device);
+  std::vector<Unit> all = build_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x,
+                                      opt_.periodic_y, opt_.edge_weight, cap);
+  L.H = 0;
+  for (const Unit& u : all) L.H = std::max(L.H, u.h);
+  if (all.size() > (size_t)(1 << 30)) throw std::runtime_error("too many work units");
+  std::vector<Unit> in, bd;
+  for (const Unit& u : all) {
+    const int64_t y0 = (int64_t)u.strip * wout, y1 = std::min(g.ycell, y0 + wout);
     const bool left = y0 - K < 0, right = y1 + K > g.ycell;
-    for (int64_t q = 0; q < nsegs; ++q) {
-      const int64_t x0 = q * L.H, x1 = std::min(g.xcell, x0 + L.H);
-      const bool top = x0 - K < 0, bot = x1 + K > g.xcell;
-      const bool needs_halo = (top && peer[kN]) || (bot && peer[kS]) || (left && peer[kW]) || (right && peer[kE]) ||
-                              (top && left && peer[kNW]) || (top && right && peer[kNE]) ||
-                              (bot && left && peer[kSW]) || (bot && right && peer[kSE]);
-      Unit u{(int)s, (int)q};
-      all.push_back(u);
-      (needs_halo ? bd : in).push_back(u);
-    }
+    const int64_t x0 = u.x0, x1 = u.x0 + u.h;
+    const bool top = x0 - K < 0, bot = x1 + K > g.xcell;
+    const bool needs_halo = (top && peer[kN]) || (bot && peer[kS]) || (left && peer[kW]) || (right && peer[kE]) ||
+                            (top && left && peer[kNW]) || (top && right && peer[kNE]) ||
+                            (bot && left && peer[kSW]) || (bot && right && peer[kSE]);
+    (needs_halo ? bd : in).push_back(u);
   }
+  // The boundary list runs after the halo arrives: order both lists edge-units-first so the
+  // longer waves start first.
+  auto edge_first = [](const Unit& a, const Unit& b) { return (a.flags != 0) > (b.flags != 0); };
+  std::stable_sort(in.begin(), in.end(), edge_first);
+  std::stable_sort(bd.begin(), bd.end(), edge_first);
+  all = in;
+  all.insert(all.end(), bd.begin(), bd.end());
   L.n_all = (int)all.size();
   L.n_interior = (int)in.size();
   L.n_boundary = (int)bd.size();
@@ -216,7 +221,6 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which) {
   StreamArgs a;
   a.src = tl.buf[tl.cur];
   a.dst = tl.buf[1 - tl.cur];
-  a.H = L.H;
   a.R = (int)lead_cols(K);
   a.wout = (int)strip_out_cols(K);
   a.pitch = g.pitch;
@@ -234,6 +238,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which) {
   a.per_x = opt_.periodic_x;
   a.per_y = opt_.periodic_y;
   a.partials = tl.partials;
+  a.dummy = d_dummy_;
   if (which == 0) {
     a.units = L.d_all;
     a.nunits = L.n_all;

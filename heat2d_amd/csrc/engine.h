@@ -48,6 +48,8 @@ struct EngineOptions {
   double cx = kCxDouble, cy = kCxDouble;
   int tblock = 8;          // max fused steps per chunk (= halo depth)
   int rows_per_wave = 0;   // H; 0 = automatic
+  double edge_weight = 1.2;  // relative cost of a global-edge work unit (load balance)
+  int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   bool convergence = false;
   int64_t interval = 20;
   double sensitivity = 0.1;
@@ -85,7 +87,8 @@ class Engine {
   int halo_depth() const { return G_; }
   bool on_gpu() const { return opt_.device >= 0; }
   bool has_exchange() const { return has_exchange_; }
-  int rows_per_wave(int K) const;
+  int rows_per_wave(int K) const;  // largest unit height for depth K (tile 0)
+  int num_units(int K) const;      // work units (waves) per chunk of depth K, all tiles
   int64_t steps_done() const { return steps_done_; }
   uintptr_t stream_handle() const { return (uintptr_t)compute_; }
 
@@ -159,6 +162,7 @@ class Engine {
   double* d_resid_ = nullptr;       // [num_tiles] + 1 total
   double* h_resid_ = nullptr;       // pinned
   long long* d_lds_steps_ = nullptr;
+  float* d_dummy_ = nullptr;        // sink for the streaming kernel's non-output lanes
   float* d_send_ = nullptr;
   float* d_recv_ = nullptr;
   int64_t stage_cap_ = 0;

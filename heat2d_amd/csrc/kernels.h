@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "h2d_common.h"
 
@@ -21,11 +22,25 @@
 
 namespace h2d {
 
-// Work unit of the streaming kernel: (strip index, row-segment index).
+// Work unit of the streaming kernel: one wave = one 256-column strip × rows [x0, x0+h).
+// flags: kEdgeCols — a column of the strip's window is a global edge / outside the grid;
+//        kEdgeRows — a row of the unit's K-cone is.  Computed on the host (unit_edge_flags).
 struct Unit {
   int strip;
-  int seg;
+  int x0;
+  int h;
+  int flags;
 };
+constexpr int kEdgeCols = 1, kEdgeRows = 2;
+
+int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t y0, bool fixed, bool per_x, bool per_y);
+// Cut a tile into work units for depth K: ~H rows per unit, edge units shortened by
+// `edge_weight` so that every wave finishes at about the same time (one wave round).
+// H > 0 fixes the rows of a plain unit; H == 0 sizes units to fill `capacity` resident waves.
+std::vector<Unit> build_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y,
+                              double edge_weight, int64_t capacity);
+// Resident waves of the streaming kernel on `device` (occupancy query × CUs × 4 waves/block).
+int64_t stream_wave_capacity(int K, int precision, int device);
 
 // Arguments of the temporally-blocked streaming stencil.
 struct StreamArgs {
@@ -33,7 +48,6 @@ struct StreamArgs {
   float* dst;
   const Unit* units;
   int nunits;
-  int H;       // output rows per unit
   int wout;    // output columns per strip (256 - 2R)
   int R;       // column lead (round_up(K,4))
   int64_t pitch, G, PL;
@@ -43,6 +57,7 @@ struct StreamArgs {
   int fixed;
   int per_x, per_y;
   double* partials;  // per-unit residual partial sums (only read by the RESID variant)
+  float* dummy;      // >= 256 floats: store target of non-output lanes in the branch-free path
 };
 
 // Largest K with a compiled streaming kernel.
@@ -71,4 +86,6 @@ void launch_lds_solver(const float* in, int64_t in_pitch, float* out, int64_t ou
 namespace h2d {
 template <int K>
 void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s);
+template <int K>
+int stream_blocks_per_cu(bool f32, bool resid);
 }  // namespace h2d

@@ -171,6 +171,111 @@ __global__ __launch_bounds__(1024) void lds_solver_kernel(const float* __restric
 #define H2D_EXTERN(K) extern template void launch_stream_k<K>(const StreamArgs&, bool, bool, hipStream_t);
 H2D_K_LIST(H2D_EXTERN)
 #undef H2D_EXTERN
+#define H2D_EXTERN2(K) extern template int stream_blocks_per_cu<K>(bool, bool);
+H2D_K_LIST(H2D_EXTERN2)
+#undef H2D_EXTERN2
+
+int64_t stream_wave_capacity(int K, int precision, int device) {
+  int bpc = 1;
+  const bool f32 = precision == kFp32;
+  switch (K) {
+#define H2D_CASE(KK) case KK: bpc = stream_blocks_per_cu<KK>(f32, false); break;
+    H2D_K_LIST(H2D_CASE)
+#undef H2D_CASE
+    default: break;
+  }
+  int cus = 256;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, device) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
+  return (int64_t)bpc * cus * 4;
+}
+
+int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t y0, bool fixed, bool per_x, bool per_y) {
+  int f = 0;
+  if (!per_y) {
+    const int64_t lo = g.gy0 + y0 - lead_cols(K), hi = lo + kWaveCols - 1;  // the wave's column window
+    const bool sp = fixed ? ((lo <= 0 && 0 <= hi) || (lo <= g.NY - 1 && g.NY - 1 <= hi)) : (lo < 0 || hi >= g.NY);
+    if (sp) f |= kEdgeCols;
+  }
+  if (!per_x) {
+    const int64_t lo = g.gx0 + x0 - K, hi = g.gx0 + x0 + h + K - 1;  // the unit's row cone
+    const bool sp = fixed ? ((lo <= 0 && 0 <= hi) || (lo <= g.NX - 1 && g.NX - 1 <= hi)) : (lo < 0 || hi >= g.NX);
+    if (sp) f |= kEdgeRows;
+  }
+  return f;
+}
+
+std::vector<Unit> build_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y,
+                              double edge_weight, int64_t capacity) {
+  std::vector<Unit> v;
+  const int64_t wout = strip_out_cols(K);
+  const int64_t nstrips = (g.ycell + wout - 1) / wout;
+  const double w = std::max(1.0, edge_weight);
+  // A unit of h rows costs ~ (h + K) wave-row-steps (the 2K-row prologue primes K levels);
+  // an edge unit costs w times more per row.  For a target unit cost U a plain strip uses
+  // h = U - K rows per unit and an edge strip / edge row block h = U/w - K.
+  struct StripInfo {
+    bool col_edge;
+    bool top_edge, bot_edge;
+  };
+  std::vector<StripInfo> info((size_t)nstrips);
+  for (int64_t s = 0; s < nstrips; ++s) {
+    const int64_t y0 = s * wout;
+    info[s].col_edge = unit_edge_flags(g, K, 0, 1, y0, fixed, true, per_y) & kEdgeCols;
+    info[s].top_edge = unit_edge_flags(g, K, 0, 1, y0, fixed, per_x, true) & kEdgeRows;
+    info[s].bot_edge = unit_edge_flags(g, K, g.xcell - 1, 1, y0, fixed, per_x, true) & kEdgeRows;
+  }
+  auto rows_for = [&](double U, bool edge) { return std::max<int64_t>(1, (int64_t)(edge ? U / w - K : U - K)); };
+  auto plan = [&](double U, std::vector<Unit>* out) -> int64_t {
+    int64_t count = 0;
+    for (int64_t s = 0; s < nstrips; ++s) {
+      const int64_t y0 = s * wout;
+      std::vector<std::pair<int64_t, int64_t>> segs;
+      auto split = [&](int64_t a, int64_t b, int64_t target) {
+        const int64_t len = b - a;
+        if (len <= 0) return;
+        const int64_t n = (len + target - 1) / target;
+        for (int64_t i = 0; i < n; ++i) segs.emplace_back(a + len * i / n, len * (i + 1) / n - len * i / n);
+      };
+      if (info[s].col_edge) {
+        split(0, g.xcell, rows_for(U, true));
+      } else {
+        const int64_t he = rows_for(U, true), hn = rows_for(U, false);
+        int64_t top = info[s].top_edge ? std::min<int64_t>(g.xcell, he) : 0;
+        int64_t bot = info[s].bot_edge ? std::max<int64_t>(top, g.xcell - he) : g.xcell;
+        split(0, top, he);
+        split(top, bot, hn);
+        split(bot, g.xcell, he);
+      }
+      count += (int64_t)segs.size();
+      if (out)
+        for (auto& sg : segs)
+          out->push_back(Unit{(int)s, (int)sg.first, (int)sg.second,
+                              unit_edge_flags(g, K, sg.first, sg.second, y0, fixed, per_x, per_y)});
+    }
+    return count;
+  };
+  double U;
+  if (H > 0) {
+    U = (double)(H + K);
+  } else {
+    // Smallest unit cost whose unit count fits one resident round (capacity waves); never
+    // shorter than 16 rows (the prologue would dominate).
+    double lo = 16.0 + K, hi = (double)(g.xcell + K) * w + 1.0;
+    if (plan(lo, nullptr) <= capacity) {
+      hi = lo;
+    } else {
+      for (int it = 0; it < 60 && hi - lo > 0.5; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (plan(mid, nullptr) <= capacity) hi = mid;
+        else lo = mid;
+      }
+    }
+    U = hi;
+  }
+  plan(U, &v);
+  return v;
+}
 
 bool stream_k_supported(int K) {
   switch (K) {

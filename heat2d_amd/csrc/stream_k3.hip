@@ -3,4 +3,5 @@
 
 namespace h2d {
 template void launch_stream_k<3>(const StreamArgs&, bool, bool, hipStream_t);
+template int stream_blocks_per_cu<3>(bool, bool);
 }  // namespace h2d

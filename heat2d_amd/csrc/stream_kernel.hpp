@@ -1,32 +1,34 @@
-// heat2d_amd — hand-written CDNA4 (gfx950) HIP kernels.
+// heat2d_amd — the streaming, temporally-blocked 5-point stencil for CDNA4 (gfx950).
 //
-// The hot kernel is `stream_kernel<K,...>`: a register-streaming, temporally-blocked 5-point
-// Jacobi stencil.  Device equivalent of the reference's update loops
-// (grad1612_cuda_heat.cu:55-62, grad1612_mpi_heat.c:238-259, mpi_heat2Dn.c:225-237), but
-// designed for the CDNA4 execution model rather than translated:
+// Device equivalent of the reference's update loops (grad1612_cuda_heat.cu:55-62,
+// grad1612_mpi_heat.c:238-259, mpi_heat2Dn.c:225-237), designed for the CDNA4 execution model
+// rather than translated:
 //
 //   * one wave64 owns a 256-column strip (4 contiguous fp32 per lane -> one 1 KiB
 //     global_load_dwordx4 per row, fully coalesced) and walks DOWN the grid row by row;
 //   * K time levels are kept in registers as a 2-row window per level ("2.5-D blocking"):
-//     each input row is read from HBM / Infinity Cache once and each output row written
-//     once per K steps, so memory traffic per cell-step is 8/K bytes;
-//   * the east/west neighbours come from the adjacent lanes through DPP wave_shr/wave_shl
-//     (no LDS, no barriers — waves are fully independent);
-//   * the strip's column lead R = round_up(K,4) absorbs the K-deep dependency cone, so a
-//     wave needs no data from any other wave; the row cone is covered by a K-row prologue;
-//   * global-edge handling (fixed Dirichlet edges, zero ring, periodic wrap) is a
-//     wave-uniform branch: strips away from the domain edge run the mask-free body.
+//     each input row is read once and each output row written once per K steps, so memory
+//     traffic per cell-step is 8/K bytes;
+//   * east/west neighbours come from the adjacent lanes through DPP wave_shr/wave_shl (no LDS,
+//     no barriers — waves are fully independent);
+//   * the strip's column lead R = round_up(K,4) absorbs the K-deep dependency cone; the row
+//     cone is a 2K-row prologue that is unrolled at compile time (no runtime checks);
+//   * the steady state is straight-line code (4 rows × K levels, no branches), so the
+//     scheduler overlaps the level chains of consecutive rows;
+//   * global-edge handling (fixed Dirichlet edges, zero ring, periodic wrap, partial stores)
+//     is a separate branch-free body (selects, per-element store redirection) chosen once per
+//     wave; waves away from the domain edge run the mask-free body.
 //
-// The kernel is fp64-VALU bound in the bit-exact `ref` precision (11 fp64-rate ops per cell:
-// the reference evaluates its update in double) and Infinity-Cache/HBM bound in
-// the fp32 precision.  No MFMA: a 5-point stencil has no dot-product of depth >= 16, and the
-// bit-exact contract forbids the FMA contraction an MFMA formulation would impose.
+// Numerics: the ref precision evaluates the reference's double expression with its exact
+// rounding sequence.  `fl(s+n - 2c)` is computed as fma(-2, c, s+n): 2c is
+// exact in double, so the fused form rounds once on the same exact value — bit-identical,
+// one fp64 op less (10 fp64-rate ops per cell).  No MFMA: a 5-point stencil has no
+// dot-product of depth >= 16 and the contract forbids the contraction it would impose.
 //
 // Included by the per-K translation units stream_k*.hip (compiled in parallel); every TU is
-// compiled with -ffp-contract=off (bit-exactness of the ref path).
+// compiled with -ffp-contract=off.
 #pragma once
 #include "kernels.h"
-
 
 namespace h2d {
 namespace {
@@ -44,12 +46,21 @@ struct Coef {
   float cxf, cyf;
 };
 
+// Device cell update; identical values to update_ref / update_f32 (h2d_common.h).
 template <bool F32>
 __device__ __forceinline__ float cell(float c, float n, float s, float w, float e, const Coef& k) {
+  const float sn = s + n;
+  const float ew = e + w;
   if constexpr (F32) {
-    return update_f32(c, n, s, w, e, k.cxf, k.cyf);
+    const float r = __builtin_fmaf(k.cxf, __builtin_fmaf(-2.0f, c, sn), c);
+    return __builtin_fmaf(k.cyf, __builtin_fmaf(-2.0f, c, ew), r);
   } else {
-    return update_ref(c, n, s, w, e, k.cx, k.cy);
+    const double dc = (double)c;
+    const double t1 = __builtin_fma(-2.0, dc, (double)sn);  // == fl(sn - 2c): 2c is exact
+    const double t4 = __builtin_fma(-2.0, dc, (double)ew);
+    double r = dc + k.cx * t1;
+    r = r + k.cy * t4;
+    return (float)r;
   }
 }
 
@@ -69,93 +80,98 @@ __device__ __forceinline__ float4 row_update(const float4& P, const float4& C, c
 struct LaneCtx {
   int64_t gxb;     // global row of stream input index 0
   int64_t NX;
-  int fixed, per_x;
-  int cm0, cm1, cm2, cm3;  // per-column modes of this lane's 4 columns
-  float* out;      // dst at (output row 0 of the unit, this lane's first column)
-  int64_t pitch;
-  int nst;         // number of this lane's columns that are stored (0..4)
+  bool m0, m1, m2, m3;  // per-column mask: fixed -> hold (global edge), ghost-zero -> zero (outside)
+  float* sout;     // real output pointer (lanes in the output range), or a dummy slot
+  int64_t spitch;  // row pitch of sout (0 for the dummy slot)
+  bool st0, st1, st2, st3;  // element is an owned output cell (residual accounting)
 };
-
-__device__ __forceinline__ int row_mode(int64_t gr, const LaneCtx& c) {
-  if (c.per_x) return 0;
-  if (gr < 0 || gr >= c.NX) return 2;
-  if (c.fixed && (gr == 0 || gr == c.NX - 1)) return 1;
-  return 0;
-}
-
-__device__ __forceinline__ float col_sel(int m, float o, float hold) { return m == 0 ? o : (m == 1 ? hold : 0.0f); }
-
-template <bool EDGE>
-__device__ __forceinline__ float4 apply_modes(float4 o, const float4& C, int rm, const LaneCtx& c) {
-  if (rm == 2) return make_float4(0.f, 0.f, 0.f, 0.f);
-  if (rm == 1) return C;
-  if constexpr (EDGE) {
-    o.x = col_sel(c.cm0, o.x, C.x);
-    o.y = col_sel(c.cm1, o.y, C.y);
-    o.z = col_sel(c.cm2, o.z, C.z);
-    o.w = col_sel(c.cm3, o.w, C.w);
-  }
-  return o;
-}
-
-__device__ __forceinline__ void store_out(float* op, const float4& o, int nst) {
-  if (nst == 4) {
-    *reinterpret_cast<float4*>(op) = o;
-  } else if (nst > 0) {
-    op[0] = o.x;
-    if (nst > 1) op[1] = o.y;
-    if (nst > 2) op[2] = o.z;
-  }
-}
 
 __device__ __forceinline__ double sq_diff(float a, float b) {
   const double d = (double)a - (double)b;
   return d * d;
 }
 
-// Process stream input row `ir` (level-0 value `cur`) through all K levels.
+// Branch-free global-edge masks (EDGE bit 0: columns, bit 1: rows).  Fixed edges hold their
+// previous value; in ghost-zero mode cells outside the grid stay 0.  (In fixed mode cells
+// outside the grid may hold anything: the held edge row/column separates them from the
+// interior.)  Row conditions are wave-uniform.
+template <int EDGE, bool FIXED>
+__device__ __forceinline__ float4 apply_edge(float4 o, const float4& C, int64_t gr, const LaneCtx& c) {
+  if constexpr ((EDGE & 1) != 0) {
+    if constexpr (FIXED) {
+      o.x = c.m0 ? C.x : o.x;
+      o.y = c.m1 ? C.y : o.y;
+      o.z = c.m2 ? C.z : o.z;
+      o.w = c.m3 ? C.w : o.w;
+    } else {
+      o.x = c.m0 ? 0.0f : o.x;
+      o.y = c.m1 ? 0.0f : o.y;
+      o.z = c.m2 ? 0.0f : o.z;
+      o.w = c.m3 ? 0.0f : o.w;
+    }
+  }
+  if constexpr ((EDGE & 2) != 0) {
+    // per component: a select of a whole float4 aggregate is lowered through scratch memory
+    if constexpr (FIXED) {
+      const bool r = gr == 0 || gr == c.NX - 1;
+      o.x = r ? C.x : o.x;
+      o.y = r ? C.y : o.y;
+      o.z = r ? C.z : o.z;
+      o.w = r ? C.w : o.w;
+    } else {
+      const bool r = gr < 0 || gr >= c.NX;
+      o.x = r ? 0.0f : o.x;
+      o.y = r ? 0.0f : o.y;
+      o.z = r ? 0.0f : o.z;
+      o.w = r ? 0.0f : o.w;
+    }
+  }
+  return o;
+}
+
+// Process stream input row `ir` (level-0 value `cur`) through levels 1..TMAX (TMAX <= K).
 // Slot parity P = ir & 1: S[l][P] holds level-l row (ir-l-2), S[l][1-P] holds row (ir-l-1).
-template <int K, bool F32, bool EDGE, bool RESID, int P, bool CHECK>
+// Level t computes row (ir - t) of level t.  Level K writes output row ir - 2K (unit-relative).
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, int P, int TMAX>
 __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int ir, const LaneCtx& c, const Coef& k,
                                             double& racc) {
 #pragma unroll
   for (int t = 1; t <= K; ++t) {
-    if constexpr (CHECK) {
-      if (ir < 2 * t) {  // level t not primed yet (wave-uniform); no early exit: keep the loop unrollable
-        if (ir >= 2 * (t - 1)) S[t - 1][P] = cur;
-        continue;
-      }
+    if (t > TMAX) {
+      if (t - 1 <= TMAX) S[t - 1][P] = cur;  // save the last active level's new row
+      continue;
     }
     const float4 prv = S[t - 1][P];
     const float4 mid = S[t - 1][1 - P];
     float4 o = row_update<F32>(prv, mid, cur, k);
-    o = apply_modes<EDGE>(o, mid, row_mode(c.gxb + ir - t, c), c);
+    if constexpr (EDGE != 0) o = apply_edge<EDGE, FIXED>(o, mid, c.gxb + ir - t, c);
     S[t - 1][P] = cur;
     if (t == K) {
-      float* op = c.out + (int64_t)(ir - 2 * K) * c.pitch;
-      store_out(op, o, c.nst);
+      const int64_t orow = ir - 2 * K;
+      *reinterpret_cast<float4*>(c.sout + orow * c.spitch) = o;
       if constexpr (RESID) {
-        if (c.nst > 0) racc += sq_diff(o.x, mid.x);
-        if (c.nst > 1) racc += sq_diff(o.y, mid.y);
-        if (c.nst > 2) racc += sq_diff(o.z, mid.z);
-        if (c.nst > 3) racc += sq_diff(o.w, mid.w);
+        racc += c.st0 ? sq_diff(o.x, mid.x) : 0.0;
+        racc += c.st1 ? sq_diff(o.y, mid.y) : 0.0;
+        racc += c.st2 ? sq_diff(o.z, mid.z) : 0.0;
+        racc += c.st3 ? sq_diff(o.w, mid.w) : 0.0;
       }
     }
     cur = o;
   }
 }
 
-#define H2D_SUBSTEP(D, CHECK, LIMIT)                                                      \
-  {                                                                                       \
-    const int ir = ir0 + (D);                                                             \
-    if (ir < (LIMIT)) {                                                                   \
-      const float4 nw = pf[D];                                                            \
-      pf[D] = rowp[(int64_t)min(ir + 4, n - 1) * pitch4];                                 \
-      process_row<K, F32, EDGE, RESID, (D)&1, CHECK>(S, nw, ir, c, k, racc);              \
-    }                                                                                     \
+// Prologue row IR (compile-time): levels t <= IR/2 are primed.
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, int IR>
+__device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4* __restrict__ rowp, int64_t pitch4,
+                                         const LaneCtx& c, const Coef& k, double& racc) {
+  if constexpr (IR < 2 * K) {
+    const float4 v = rowp[(int64_t)IR * pitch4];
+    process_row<K, F32, EDGE, FIXED, RESID, IR & 1, IR / 2>(S, v, IR, c, k, racc);
+    prologue<K, F32, EDGE, FIXED, RESID, IR + 1>(S, rowp, pitch4, c, k, racc);
   }
+}
 
-template <int K, bool F32, bool EDGE, bool RESID>
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID>
 __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, int64_t pitch4, int n, const LaneCtx& c,
                                          const Coef& k, double& racc) {
   float4 S[K][2];
@@ -164,31 +180,43 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, int64_
     S[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
     S[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // n = h + 2K >= 2K + 1: the prologue rows all exist.  Prefetch the first steady rows first.
   float4 pf[4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(d, n - 1) * pitch4];
+  for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(2 * K + d, n - 1) * pitch4];
+  prologue<K, F32, EDGE, FIXED, RESID, 0>(S, rowp, pitch4, c, k, racc);
 
-  const int npro = min(n, (2 * K + 3) & ~3);
-  int ir0 = 0;
-  for (; ir0 < npro; ir0 += 4) {  // prologue: levels start one by one
-    H2D_SUBSTEP(0, true, npro)
-    H2D_SUBSTEP(1, true, npro)
-    H2D_SUBSTEP(2, true, npro)
-    H2D_SUBSTEP(3, true, npro)
+  int ir0 = 2 * K;  // even: slot parity of sub-step d is d & 1
+#define H2D_STEADY(D)                                                        \
+  {                                                                          \
+    const float4 nw = pf[D];                                                 \
+    pf[D] = rowp[(int64_t)min(ir0 + (D) + 4, n - 1) * pitch4];               \
+    process_row<K, F32, EDGE, FIXED, RESID, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
-  for (; ir0 < n; ir0 += 4) {  // steady state: every level active, no checks
-    H2D_SUBSTEP(0, false, n)
-    H2D_SUBSTEP(1, false, n)
-    H2D_SUBSTEP(2, false, n)
-    H2D_SUBSTEP(3, false, n)
+  for (; ir0 + 4 <= n; ir0 += 4) {
+    H2D_STEADY(0)
+    H2D_STEADY(1)
+    H2D_STEADY(2)
+    H2D_STEADY(3)
   }
+#undef H2D_STEADY
+  // tail: at most 3 rows
+  if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, 0, K>(S, pf[0], ir0, c, k, racc);
+  if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
+  if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
 }
-#undef H2D_SUBSTEP
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+template <int K, bool F32, bool RESID, int EDGE>
+__device__ __forceinline__ void run_edge(const float4* rowp, int64_t pitch4, int n, const LaneCtx& c, const Coef& k,
+                                         double& racc, bool fixed) {
+  if (fixed) run_unit<K, F32, EDGE, true, RESID>(rowp, pitch4, n, c, k, racc);
+  else run_unit<K, F32, EDGE, false, RESID>(rowp, pitch4, n, c, k, racc);
 }
 
 template <int K, bool F32, bool RESID>
@@ -199,35 +227,43 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const int lane = (int)(threadIdx.x & 63);
   const Unit u = a.units[w];
   const int64_t y0 = (int64_t)u.strip * a.wout;
-  const int64_t x0 = (int64_t)u.seg * a.H;
-  const int h = (int)min((int64_t)a.H, a.xcell - x0);
+  const int64_t x0 = u.x0;
+  const int h = u.h;
   const int64_t cb = y0 - a.R + 4 * lane;
 
   LaneCtx c;
   c.gxb = a.gx0 + x0 - K;
   c.NX = a.NX;
-  c.fixed = a.fixed;
-  c.per_x = a.per_x;
   const int64_t gc = a.gy0 + cb;
-  c.cm0 = dim_mode(gc + 0, a.NY, a.per_y != 0, a.fixed != 0);
-  c.cm1 = dim_mode(gc + 1, a.NY, a.per_y != 0, a.fixed != 0);
-  c.cm2 = dim_mode(gc + 2, a.NY, a.per_y != 0, a.fixed != 0);
-  c.cm3 = dim_mode(gc + 3, a.NY, a.per_y != 0, a.fixed != 0);
-  const bool lane_special = (c.cm0 | c.cm1 | c.cm2 | c.cm3) != 0;
-  const bool in_out = (cb >= y0) && (cb + 4 <= y0 + a.wout);
-  c.nst = in_out ? (int)max((int64_t)0, min((int64_t)4, a.ycell - cb)) : 0;
-  c.pitch = a.pitch;
-  c.out = a.dst + (a.G + x0) * a.pitch + a.PL + cb;
+  const bool fixed = a.fixed != 0;
+  auto colmask = [&](int64_t q) {
+    return fixed ? (q == 0 || q == a.NY - 1) : (q < 0 || q >= a.NY);
+  };
+  c.m0 = colmask(gc + 0);
+  c.m1 = colmask(gc + 1);
+  c.m2 = colmask(gc + 2);
+  c.m3 = colmask(gc + 3);
+  // Lanes in the output range store a full float4 (columns past ycell land in the ghost /
+  // pad columns inside the pitch and hold valid cone values there); others hit a dummy slot.
+  const bool in_out = (cb >= y0) && (cb + 4 <= y0 + a.wout) && (cb < a.ycell);
+  float* out = a.dst + (a.G + x0) * a.pitch + a.PL + cb;
+  c.sout = in_out ? out : a.dummy + 4 * lane;
+  c.spitch = in_out ? a.pitch : 0;
+  c.st0 = in_out;
+  c.st1 = in_out && cb + 1 < a.ycell;
+  c.st2 = in_out && cb + 2 < a.ycell;
+  c.st3 = in_out && cb + 3 < a.ycell;
 
   const float4* rowp = reinterpret_cast<const float4*>(a.src + (a.G + x0 - K) * a.pitch + a.PL + cb);
   const int64_t pitch4 = a.pitch >> 2;
   const int n = h + 2 * K;
   Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
   double racc = 0.0;
-  if (__any(lane_special)) {
-    run_unit<K, F32, true, RESID>(rowp, pitch4, n, c, k, racc);
-  } else {
-    run_unit<K, F32, false, RESID>(rowp, pitch4, n, c, k, racc);
+  switch (u.flags & 3) {
+    case 0: run_unit<K, F32, 0, false, RESID>(rowp, pitch4, n, c, k, racc); break;
+    case 1: run_edge<K, F32, RESID, 1>(rowp, pitch4, n, c, k, racc, fixed); break;
+    case 2: run_edge<K, F32, RESID, 2>(rowp, pitch4, n, c, k, racc, fixed); break;
+    default: run_edge<K, F32, RESID, 3>(rowp, pitch4, n, c, k, racc, fixed); break;
   }
   if constexpr (RESID) {
     racc = wave_sum(racc);
@@ -244,6 +280,16 @@ void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s) {
   if (f32) fn = resid ? stream_kernel<K, true, true> : stream_kernel<K, true, false>;
   else fn = resid ? stream_kernel<K, false, true> : stream_kernel<K, false, false>;
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, a);
+}
+
+template <int K>
+int stream_blocks_per_cu(bool f32, bool resid) {
+  void (*fn)(StreamArgs);
+  if (f32) fn = resid ? stream_kernel<K, true, true> : stream_kernel<K, true, false>;
+  else fn = resid ? stream_kernel<K, false, true> : stream_kernel<K, false, false>;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), 256, 0) != hipSuccess) return 1;
+  return nb > 0 ? nb : 1;
 }
 
 }  // namespace h2d
