@@ -36,7 +36,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--n", type=int, default=4096, help="grid side (per GPU for weak scaling)")
+    ap.add_argument("--side", type=int, default=4096, help="grid side (per GPU for weak scaling)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--precision", choices=("ref", "fp32"), default="ref")
     ap.add_argument("--boundary", choices=("fixed", "ghost-zero"), default="fixed")
@@ -45,6 +45,8 @@ def main() -> int:
     ap.add_argument("--transport", choices=("auto", "rccl", "torch"), default="auto")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--repeat", type=int, default=1, help="timed repetitions (best reported)")
+    ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
+                    help="cpu: rehearsal of the distributed contract on the host (gloo), not a benchmark")
     a = ap.parse_args()
 
     import torch
@@ -59,29 +61,34 @@ def main() -> int:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     gx, gy = auto_grid(world)
     if a.scaling == "weak":
-        nx, ny = a.n * gx, a.n * gy
+        nx, ny = a.side * gx, a.side * gy
     else:
-        nx = ny = a.n
+        nx = ny = a.side
     cfg = Config(preset="heat2d", nx=nx, ny=ny, steps=a.steps, gridx=gx, gridy=gy, boundary=a.boundary,
-                 precision=a.precision, init="exact", output="none", device="gpu", transport=a.transport,
+                 precision=a.precision, init="exact", output="none", device=a.device, transport=a.transport,
                  tblock=a.tblock, rows_per_wave=a.rows_per_wave, overlap=not a.no_overlap, quiet=True,
                  report="grad", text_style="grad")
     s = Solver(cfg, ctx)
 
+    on_gpu = a.device == "gpu"
+
     def sync_barrier():
-        torch.cuda.synchronize()
+        if on_gpu:
+            torch.cuda.synchronize()
         ctx.barrier()
-        torch.cuda.synchronize()
+        if on_gpu:
+            torch.cuda.synchronize()
 
     # warm-up (untimed): also builds every lazy structure and warms caches
+    run = s.run_steps
     if a.warmup > 0:
-        s.engine.run(a.warmup)
+        run(a.warmup)
     best = None
     res = None
     for _ in range(max(1, a.repeat)):
         sync_barrier()
         t0 = time.perf_counter()
-        res = s.engine.run(a.steps)
+        res = run(a.steps)
         sync_barrier()
         dt = ctx.allreduce_max(time.perf_counter() - t0)
         best = dt if best is None else min(best, dt)

@@ -160,15 +160,18 @@ class Solver:
         st["path"] = "external"
         return st
 
+    def run_steps(self, steps: int) -> dict:
+        """Advance `steps` steps with whichever loop the transport needs (no barriers/timing)."""
+        if self.transport == native().TRANSPORT_EXTERNAL and self.engine.has_exchange():
+            return self._python_loop(steps)
+        return self.engine.run(steps)
+
     def run(self, steps: Optional[int] = None) -> RunResult:
         steps = self.cfg.steps if steps is None else steps
         self.ctx.barrier()
         self.engine.synchronize()
         t0 = time.perf_counter()
-        if self.transport == native().TRANSPORT_EXTERNAL and self.engine.has_exchange():
-            st = self._python_loop(steps)
-        else:
-            st = self.engine.run(steps)
+        st = self.run_steps(steps)
         self.engine.synchronize()
         local = time.perf_counter() - t0
         elapsed = self.ctx.allreduce_max(local)

@@ -1,0 +1,114 @@
+"""Multi-process runs on the CPU: torch.distributed (gloo) with world_size > 1.
+
+Each rank owns one tile and exchanges its K-deep, 8-neighbour halo through
+``TorchHaloExchanger`` (the engine's exchange plan); the global binary written with per-rank
+pwrite must equal the single-process oracle bit for bit — the decomposition-invariance
+oracle of SURVEY.md §2.9.  Launched exactly like the driver launches the bench
+(``python -m torch.distributed.run --master-addr 127.0.0.1``).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def torchrun(n, args, cwd, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m", "heat2d_amd", "--device", "cpu",
+           *args]
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["OMP_NUM_THREADS"] = "1"
+    env["HEAT2D_NO_BUILD"] = "1"
+    r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def read_grid(path, nx, ny):
+    return np.fromfile(path, dtype=np.float32).reshape(nx, ny)
+
+
+@pytest.mark.parametrize("n,gx,gy,boundary", [(2, 2, 1, "fixed"), (2, 1, 2, "ghost-zero"), (4, 2, 2, "fixed"),
+                                              (3, 3, 1, "ghost-zero")])
+def test_gloo_ranks_match_oracle(native, tmp_path, n, gx, gy, boundary):
+    nx, ny, steps = 53, 47, 37
+    out = torchrun(n, ["--nx", str(nx), "--ny", str(ny), "--steps", str(steps), "--gridx", str(gx), "--gridy", str(gy),
+                       "--boundary", boundary, "--output", "binary", "--outdir", str(tmp_path), "--tblock", "5"],
+                   str(tmp_path))
+    assert f"Starting with {n} processes" in out
+    b = 0 if boundary == "fixed" else 1
+    ref = native.oracle_run(nx, ny, steps, boundary=b)["grid"]
+    assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
+    assert np.array_equal(read_grid(tmp_path / "initial_binary.dat", nx, ny), native.init_global(nx, ny, 0))
+
+
+def test_gloo_convergence_allreduce(native, tmp_path):
+    nx, ny = 24, 30
+    out = torchrun(2, ["--nx", str(nx), "--ny", str(ny), "--steps", "100000", "--gridx", "1", "--gridy", "2",
+                       "--convergence", "1", "--interval", "7", "--sensitivity", "0.5", "--output", "binary",
+                       "--outdir", str(tmp_path)], str(tmp_path))
+    ref = native.oracle_run(nx, ny, 100000, convergence=True, interval=7, sensitivity=0.5)
+    assert ref["converged"]
+    assert f"Exiting after {ref['steps_done']} iterations" in out
+    assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref["grid"])
+
+
+def test_gloo_periodic_blocks(native, tmp_path):
+    nx, ny, steps = 40, 36, 21
+    torchrun(4, ["--nx", str(nx), "--ny", str(ny), "--steps", str(steps), "--gridx", "2", "--gridy", "2",
+                 "--periodic", "xy", "--boundary", "ghost-zero", "--output", "binary", "--outdir", str(tmp_path)],
+             str(tmp_path))
+    ref = native.oracle_run(nx, ny, steps, boundary=1, periodic_x=True, periodic_y=True)["grid"]
+    assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
+
+
+def test_gloo_heat2dn_strips_text(native, tmp_path):
+    """Original-program personality on 3 ranks: 1-D strips, transposed text dump."""
+    nx, ny = 16, 8
+    torchrun(3, ["--preset", "heat2dn", "--nx", str(nx), "--ny", str(ny), "--outdir", str(tmp_path)], str(tmp_path))
+    from heat2d_amd.utils.io import format_text
+
+    ref = native.oracle_run(nx, ny, 100, cx=native.CX_FLOAT, cy=native.CX_FLOAT)["grid"]
+    assert (tmp_path / "final.dat").read_text() == format_text(ref, "heat2dn")
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_bench_contract_cpu_rehearsal(tmp_path, n):
+    """bench.py under torch.distributed.run: one JSON line from rank 0, whole-job value."""
+    import json
+
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["HEAT2D_NO_BUILD"] = "1"
+    args = ["--gpus", str(n), "--steps", "6", "--warmup", "2", "--side", "48", "--device", "cpu"]
+    if n == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+               "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), *args]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == n and d["steps"] == 6 and d["scaling"] == "weak"
+    gx, gy = d["config"]["grid"]
+    assert gx * gy == 48 * 48 * n
+    assert abs(d["value"] - gx * gy * 6 / d["elapsed_s"]) / d["value"] < 1e-9
