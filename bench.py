@@ -11,9 +11,12 @@ Config (BASELINE.json): 4096×4096 fp32 grid, 1000 steps, center-hot initial fie
 Numerics: the bit-exact reference expression (fp32 storage, fp64 arithmetic exactly as the
 reference's C evaluates it) unless ``--precision fp32``.
 
-Scaling: ``--scaling weak`` (default) gives every GPU a 4096×4096 tile (global grid
-4096·GRIDX × 4096·GRIDY, 2-D block decomposition, RCCL halo exchange over xGMI overlapped
-with interior compute); ``--scaling strong`` splits one 4096×4096 grid over the N GPUs.
+Scaling: ``--scaling weak`` (default) gives every GPU a 4096×4096 tile; ``--scaling strong``
+splits one 4096×4096 grid over the N GPUs.  Decomposition ``--layout rows`` (default): 1-D
+row strips (GRIDX = N, the BASELINE's "1D row decomposition with RCCL ghost-row send/recv"),
+whose few halo-dependent work units run on a second stream CONCURRENTLY with the interior
+while the K-deep ghost rows move over xGMI by RCCL send/recv; ``--layout blocks``: 2-D
+near-square blocks (e.g. 2×4).
 ``vs_baseline`` divides by the reference's best published throughput, 1.01e10 cell-updates/s
 (2560×2048, 160 MPI tasks on 20 nodes, Report.pdf p.21 Table 1 — BASELINE.md).
 """
@@ -43,6 +46,7 @@ def main() -> int:
     ap.add_argument("--tblock", type=int, default=8)
     ap.add_argument("--rows-per-wave", type=int, default=0)
     ap.add_argument("--transport", choices=("auto", "rccl", "torch"), default="auto")
+    ap.add_argument("--layout", choices=("rows", "blocks"), default="rows")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--repeat", type=int, default=1, help="timed repetitions (best reported)")
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
@@ -59,7 +63,7 @@ def main() -> int:
     world = ctx.world
     if world != a.gpus and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    gx, gy = auto_grid(world)
+    gx, gy = (world, 1) if a.layout == "rows" else auto_grid(world)
     if a.scaling == "weak":
         nx, ny = a.side * gx, a.side * gy
     else:
@@ -117,7 +121,8 @@ def main() -> int:
                 "grid_per_gpu": [nx // gx, ny // gy],
                 "global_batch": nx * ny,
                 "seq_len": a.steps,
-                "parallelism": f"blocks{gx}x{gy}" if world > 1 else "single",
+                "parallelism": (f"rows{gx}" if a.layout == "rows" else f"blocks{gx}x{gy}") if world > 1 else "single",
+                "overlap": "concurrent" if s.engine.concurrent() else ("boundary-first" if cfg.overlap else "none"),
                 "tblock": s.engine.halo_depth(),
                 "path": res["path"],
                 "transport": cfg.transport,

@@ -99,12 +99,38 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     // Build every unit list (and size the residual partials) up front: nothing is
     // allocated inside the time loop.
     for (int t = 0; t < (int)tiles_.size(); ++t) {
-      Tile& tl = tiles_[t];
-      tl.pcap = 256;
-      tl.partials = dmalloc<double>(256);
+      tiles_[t].pcap = 256;
+      tiles_[t].partials = dmalloc<double>(256);
+    }
+    // Overlap mode: run the halo-dependent boundary units CONCURRENTLY with the interior
+    // (second stream) when they are few — e.g. 1-D row decompositions — otherwise first.
+    concurrent_ = false;
+    if (has_exchange_ && opt_.overlap && opt_.concurrent != 0) {
+      if (opt_.concurrent > 0) {
+        concurrent_ = true;
+      } else {
+        int64_t nb = 0;
+        for (int t = 0; t < (int)tiles_.size(); ++t) nb += units(t, G_).n_boundary;
+        const int64_t cap = opt_.wave_capacity > 0 ? opt_.wave_capacity : stream_wave_capacity(G_, opt_.precision, opt_.device);
+        concurrent_ = nb * 8 <= cap;
+        for (auto& kv : units_) {
+          hipFree(kv.second.d_all);
+          hipFree(kv.second.d_interior);
+          hipFree(kv.second.d_boundary);
+        }
+        units_.clear();
+      }
+    }
+    if (concurrent_) {
+      H2D_HIP_CHECK(hipStreamCreateWithFlags(&bstream_, hipStreamNonBlocking));
+      for (int i = 0; i < 2; ++i) {
+        H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_i_[i], hipEventDisableTiming));
+        H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_b_[i], hipEventDisableTiming));
+      }
+    }
+    for (int t = 0; t < (int)tiles_.size(); ++t)
       for (int K = 1; K <= G_; ++K)
         if (stream_k_supported(K)) units(t, K);
-    }
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
   }
 }
@@ -136,6 +162,11 @@ Engine::~Engine() {
   hipEventDestroy(ev_halo_);
   hipEventDestroy(ev_t0_);
   hipEventDestroy(ev_t1_);
+  if (bstream_) hipStreamDestroy(bstream_);
+  for (int i = 0; i < 2; ++i) {
+    if (ev_i_[i]) hipEventDestroy(ev_i_[i]);
+    if (ev_b_[i]) hipEventDestroy(ev_b_[i]);
+  }
   hipStreamDestroy(compute_);
   hipStreamDestroy(comm_);
 }
@@ -166,33 +197,24 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   const Tile& tl = tiles_[t];
   const TileGeom& g = tl.g;
   UnitLists L;
-  const int64_t wout = strip_out_cols(K);
-  std::array<bool, kNumDirs> peer;
+  bool peer[kNumDirs];
   for (int d = 0; d < kNumDirs; ++d) peer[d] = dec_.neighbor(tl.rank, d) >= 0;
   const int64_t cap = opt_.wave_capacity > 0 ? opt_.wave_capacity : stream_wave_capacity(K, opt_.precision, opt_.device);
-  std::vector<Unit> all = build_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x,
-                                      opt_.periodic_y, opt_.edge_weight, cap);
-  L.H = 0;
-  for (const Unit& u : all) L.H = std::max(L.H, u.h);
-  if (all.size() > (size_t)(1 << 30)) throw std::runtime_error("too many work units");
-  std::vector<Unit> in, bd;
-  for (const Unit& u : all) {
-    const int64_t y0 = (int64_t)u.strip * wout, y1 = std::min(g.ycell, y0 + wout);
-    const bool left = y0 - K < 0, right = y1 + K > g.ycell;
-    const int64_t x0 = u.x0, x1 = u.x0 + u.h;
-    const bool top = x0 - K < 0, bot = x1 + K > g.xcell;
-    const bool needs_halo = (top && peer[kN]) || (bot && peer[kS]) || (left && peer[kW]) || (right && peer[kE]) ||
-                            (top && left && peer[kNW]) || (top && right && peer[kNE]) ||
-                            (bot && left && peer[kSW]) || (bot && right && peer[kSE]);
-    (needs_halo ? bd : in).push_back(u);
+  UnitPlan P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
+                          opt_.edge_weight, cap, peer, opt_.boundary_rows);
+  if (concurrent_ && !P.boundary.empty()) {
+    // boundary and interior launches are co-resident: interior units fill what is left
+    const int64_t cap_in = std::max<int64_t>(cap / 2, cap - (int64_t)P.boundary.size());
+    P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
+                   opt_.edge_weight, cap_in, peer, opt_.boundary_rows);
   }
-  // The boundary list runs after the halo arrives: order both lists edge-units-first so the
-  // longer waves start first.
-  auto edge_first = [](const Unit& a, const Unit& b) { return (a.flags != 0) > (b.flags != 0); };
-  std::stable_sort(in.begin(), in.end(), edge_first);
-  std::stable_sort(bd.begin(), bd.end(), edge_first);
-  all = in;
+  std::vector<Unit>& in = P.interior;
+  std::vector<Unit>& bd = P.boundary;
+  std::vector<Unit> all = in;
   all.insert(all.end(), bd.begin(), bd.end());
+  if (all.size() > (size_t)(1 << 30)) throw std::runtime_error("too many work units");
+  L.H = 0;
+  for (const Unit& u : in) L.H = std::max(L.H, u.h);
   L.n_all = (int)all.size();
   L.n_interior = (int)in.size();
   L.n_boundary = (int)bd.size();
@@ -214,13 +236,14 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   return units_.emplace(key, L).first->second;
 }
 
-void Engine::launch_chunk_tile(int t, int K, bool residual, int which) {
+void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, hipStream_t stream) {
   Tile& tl = tiles_[t];
   const TileGeom& g = tl.g;
   const UnitLists& L = units(t, K);
   StreamArgs a;
-  a.src = tl.buf[tl.cur];
-  a.dst = tl.buf[1 - tl.cur];
+  if (src < 0) src = tl.cur;
+  a.src = tl.buf[src];
+  a.dst = tl.buf[1 - src];
   a.R = (int)lead_cols(K);
   a.wout = (int)strip_out_cols(K);
   a.pitch = g.pitch;
@@ -250,11 +273,14 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which) {
     a.nunits = L.n_boundary;
     a.partials = tl.partials + L.n_interior;
   }
-  launch_stream(a, K, opt_.precision, residual, compute_);
-  if (residual && which != 1) {
-    // Deterministic reduction of this tile's per-wave partials into d_resid_[t].
-    launch_reduce_sum(tl.partials, L.n_all, d_resid_ + t, compute_);
-  }
+  launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
+  if (residual && which == 0) reduce_tile_residual(t, K);
+}
+
+void Engine::reduce_tile_residual(int t, int K) {
+  // Deterministic reduction of the tile's per-wave partials (interior then boundary) into d_resid_[t].
+  const UnitLists& L = units(t, K);
+  launch_reduce_sum(tiles_[t].partials, L.n_all, d_resid_ + t, compute_);
 }
 
 int Engine::next_chunk(int64_t done, int64_t total, bool* check) const {
@@ -510,37 +536,134 @@ RunStats Engine::run(int64_t steps) {
     st.chunks = 1;
   } else {
     st.path = opt_.naive ? "naive" : "stream";
-    while (steps_done_ < target) {
+    if (has_exchange_ && concurrent_ && !opt_.naive) {
+      // Concurrent pipeline (per chunk c), three streams:
+      //   B (bstream_): wait halo(c), interior(c-1) -> boundary units(c) -> evB[c&1]
+      //   C (comm_)   : wait evB[c&1] -> halo exchange of chunk c+1 (from boundary outputs)
+      //   I (compute_): wait evB[(c-1)&1] -> interior units(c) -> evI[c&1]
+      // The exchange latency is off the critical path as long as boundary + exchange
+      // fit under the interior launch.
       bool check = false;
-      const int k = next_chunk(steps_done_, target, &check);
-      if (has_exchange_) {
+      int k = next_chunk(steps_done_, target, &check);
+      H2D_HIP_CHECK(hipEventRecord(ev_i_[1], compute_));
+      H2D_HIP_CHECK(hipEventRecord(ev_b_[1], compute_));
+      if (k > 0) {
+        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_i_[1], 0));
+        do_exchange_async(k);
+        H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
+        ++st.exchanges;
+      }
+      int c = 0;
+      while (k > 0) {
+        const int p = c & 1, q = p ^ 1;
+        H2D_HIP_CHECK(hipStreamWaitEvent(bstream_, ev_halo_, 0));
+        H2D_HIP_CHECK(hipStreamWaitEvent(bstream_, ev_i_[q], 0));
+        const int src = tiles_[0].cur;
+        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2, src, bstream_);
+        H2D_HIP_CHECK(hipEventRecord(ev_b_[p], bstream_));
+        for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
+        bool check_next = false;
+        const int k_next = next_chunk(steps_done_ + k, target, &check_next);
+        if (k_next > 0) {
+          H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_b_[p], 0));
+          do_exchange_async(k_next);
+          H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
+          ++st.exchanges;
+        }
+        H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[q], 0));
+        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1, src, compute_);
+        H2D_HIP_CHECK(hipEventRecord(ev_i_[p], compute_));
+        ++st.chunks;
+        if (check) {
+          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[p], 0));
+          for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
+          st.residual = finish_residual();
+          if (st.residual < opt_.sensitivity) {
+            rollback();
+            st.converged = true;
+            break;
+          }
+        }
+        steps_done_ += k;
+        k = k_next;
+        check = check_next;
+        ++c;
+      }
+      H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
+      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
+      H2D_HIP_CHECK(hipEventRecord(ev_ready_, bstream_));
+      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
+    } else if (has_exchange_ && opt_.overlap && !opt_.naive) {
+      // Boundary-first pipeline (per chunk c):
+      //   compute: wait halo(c) -> boundary units(c) -> [event] -> interior units(c)
+      //   comm   : wait boundary(c) -> exchange the halo of chunk c+1 from the boundary outputs
+      // Boundary units are short (they gate the exchange); the exchange of chunk c+1 runs
+      // under the interior units of chunk c.
+      bool check = false;
+      int k = next_chunk(steps_done_, target, &check);
+      if (k > 0) {
         H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
         H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
         do_exchange_async(k);
         H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
         ++st.exchanges;
-        if (opt_.overlap && !opt_.naive) {
-          for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1);
-          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
-          for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2);
-          for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
-        } else {
-          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
-          advance(k, check);
+      }
+      while (k > 0) {
+        H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2);
+        H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
+        const int src = tiles_[0].cur;
+        for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
+        bool check_next = false;
+        const int k_next = next_chunk(steps_done_ + k, target, &check_next);
+        if (k_next > 0) {
+          H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+          do_exchange_async(k_next);
+          H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
+          ++st.exchanges;
         }
-      } else {
+        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1, src);
+        ++st.chunks;
+        if (check) {
+          for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
+          st.residual = finish_residual();
+          if (st.residual < opt_.sensitivity) {
+            rollback();
+            st.converged = true;
+            break;
+          }
+        }
+        steps_done_ += k;
+        k = k_next;
+        check = check_next;
+      }
+      // join the comm stream (a speculative exchange may still be in flight)
+      H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
+      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
+    } else {
+      while (steps_done_ < target) {
+        bool check = false;
+        const int k = next_chunk(steps_done_, target, &check);
+        if (has_exchange_) {
+          H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
+          H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+          do_exchange_async(k);
+          H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
+          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+          ++st.exchanges;
+        }
         advance(k, check);
-      }
-      ++st.chunks;
-      if (check) {
-        st.residual = finish_residual();
-        if (st.residual < opt_.sensitivity) {
-          rollback();
-          st.converged = true;
-          break;
+        ++st.chunks;
+        if (check) {
+          st.residual = finish_residual();
+          if (st.residual < opt_.sensitivity) {
+            rollback();
+            st.converged = true;
+            break;
+          }
         }
+        steps_done_ += k;
       }
-      steps_done_ += k;
     }
     H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
   }

@@ -50,6 +50,8 @@ struct EngineOptions {
   int rows_per_wave = 0;   // H; 0 = automatic
   double edge_weight = 1.2;  // relative cost of a global-edge work unit (load balance)
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
+  int boundary_rows = 16;     // rows per halo-dependent work unit (overlap mode)
+  int concurrent = -1;        // boundary units on a second stream: -1 auto, 0 never, 1 always
   bool convergence = false;
   int64_t interval = 20;
   double sensitivity = 0.1;
@@ -87,6 +89,7 @@ class Engine {
   int halo_depth() const { return G_; }
   bool on_gpu() const { return opt_.device >= 0; }
   bool has_exchange() const { return has_exchange_; }
+  bool concurrent() const { return concurrent_; }
   int rows_per_wave(int K) const;  // largest unit height for depth K (tile 0)
   int num_units(int K) const;      // work units (waves) per chunk of depth K, all tiles
   int64_t steps_done() const { return steps_done_; }
@@ -138,7 +141,9 @@ class Engine {
   };
 
   const UnitLists& units(int t, int K);
-  void launch_chunk_tile(int t, int K, bool residual, int which);  // which: 0 all, 1 interior, 2 boundary
+  // which: 0 all, 1 interior, 2 boundary; src: storage index read (-1: current)
+  void launch_chunk_tile(int t, int K, bool residual, int which, int src = -1, hipStream_t stream = nullptr);
+  void reduce_tile_residual(int t, int K);
   void do_exchange_async(int K);  // enqueue on comm stream
   double finish_residual();       // reduce + (rccl) all-reduce, host sync
   CopyDesc* local_descs(int K, int& n, int64_t& maxe);
@@ -153,7 +158,9 @@ class Engine {
   int64_t steps_done_ = 0;
 
   // device state
-  hipStream_t compute_ = nullptr, comm_ = nullptr;
+  hipStream_t compute_ = nullptr, comm_ = nullptr, bstream_ = nullptr;
+  hipEvent_t ev_i_[2] = {nullptr, nullptr}, ev_b_[2] = {nullptr, nullptr};
+  bool concurrent_ = false;
   hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_t0_ = nullptr, ev_t1_ = nullptr;
   std::map<std::pair<int, int>, UnitLists> units_;
   std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> local_descs_;  // (K, parity)

@@ -39,6 +39,14 @@ int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t y0,
 // H > 0 fixes the rows of a plain unit; H == 0 sizes units to fill `capacity` resident waves.
 std::vector<Unit> build_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y,
                               double edge_weight, int64_t capacity);
+// Work units of a tile split for halo overlap: `boundary` units (their K-cone reaches a ghost
+// side that has a peer; hb rows each) and `interior` units (everything else, sized to fill
+// `capacity` resident waves).  Without peers every unit is interior.
+struct UnitPlan {
+  std::vector<Unit> interior, boundary;
+};
+UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
+                    int64_t capacity, const bool* peer, int hb);
 // Resident waves of the streaming kernel on `device` (occupancy query × CUs × 4 waves/block).
 int64_t stream_wave_capacity(int K, int precision, int device);
 

@@ -205,53 +205,33 @@ int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t y0,
   return f;
 }
 
-std::vector<Unit> build_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y,
-                              double edge_weight, int64_t capacity) {
-  std::vector<Unit> v;
-  const int64_t wout = strip_out_cols(K);
-  const int64_t nstrips = (g.ycell + wout - 1) / wout;
+namespace {
+struct RowRange {
+  int64_t strip, a, b;  // rows [a, b) of strip
+  bool edge;            // costs `w` per row (global-edge masks)
+};
+
+// Cut every range into units of (nearly) equal cost, fitting `capacity` waves in one round.
+// A unit of h rows costs ~ (h + K) wave-row-steps (the 2K-row prologue primes K levels); an
+// edge unit costs w times more: target cost U -> h = U - K (plain) or U/w - K (edge).
+std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<RowRange>& ranges, int H, bool fixed,
+                              bool per_x, bool per_y, double edge_weight, int64_t capacity) {
   const double w = std::max(1.0, edge_weight);
-  // A unit of h rows costs ~ (h + K) wave-row-steps (the 2K-row prologue primes K levels);
-  // an edge unit costs w times more per row.  For a target unit cost U a plain strip uses
-  // h = U - K rows per unit and an edge strip / edge row block h = U/w - K.
-  struct StripInfo {
-    bool col_edge;
-    bool top_edge, bot_edge;
-  };
-  std::vector<StripInfo> info((size_t)nstrips);
-  for (int64_t s = 0; s < nstrips; ++s) {
-    const int64_t y0 = s * wout;
-    info[s].col_edge = unit_edge_flags(g, K, 0, 1, y0, fixed, true, per_y) & kEdgeCols;
-    info[s].top_edge = unit_edge_flags(g, K, 0, 1, y0, fixed, per_x, true) & kEdgeRows;
-    info[s].bot_edge = unit_edge_flags(g, K, g.xcell - 1, 1, y0, fixed, per_x, true) & kEdgeRows;
-  }
+  const int64_t wout = strip_out_cols(K);
   auto rows_for = [&](double U, bool edge) { return std::max<int64_t>(1, (int64_t)(edge ? U / w - K : U - K)); };
   auto plan = [&](double U, std::vector<Unit>* out) -> int64_t {
     int64_t count = 0;
-    for (int64_t s = 0; s < nstrips; ++s) {
-      const int64_t y0 = s * wout;
-      std::vector<std::pair<int64_t, int64_t>> segs;
-      auto split = [&](int64_t a, int64_t b, int64_t target) {
-        const int64_t len = b - a;
-        if (len <= 0) return;
-        const int64_t n = (len + target - 1) / target;
-        for (int64_t i = 0; i < n; ++i) segs.emplace_back(a + len * i / n, len * (i + 1) / n - len * i / n);
-      };
-      if (info[s].col_edge) {
-        split(0, g.xcell, rows_for(U, true));
-      } else {
-        const int64_t he = rows_for(U, true), hn = rows_for(U, false);
-        int64_t top = info[s].top_edge ? std::min<int64_t>(g.xcell, he) : 0;
-        int64_t bot = info[s].bot_edge ? std::max<int64_t>(top, g.xcell - he) : g.xcell;
-        split(0, top, he);
-        split(top, bot, hn);
-        split(bot, g.xcell, he);
-      }
-      count += (int64_t)segs.size();
+    for (const RowRange& r : ranges) {
+      const int64_t len = r.b - r.a;
+      if (len <= 0) continue;
+      const int64_t n = (len + rows_for(U, r.edge) - 1) / rows_for(U, r.edge);
+      count += n;
       if (out)
-        for (auto& sg : segs)
-          out->push_back(Unit{(int)s, (int)sg.first, (int)sg.second,
-                              unit_edge_flags(g, K, sg.first, sg.second, y0, fixed, per_x, per_y)});
+        for (int64_t i = 0; i < n; ++i) {
+          const int64_t s0 = r.a + len * i / n, s1 = r.a + len * (i + 1) / n;
+          out->push_back(Unit{(int)r.strip, (int)s0, (int)(s1 - s0),
+                              unit_edge_flags(g, K, s0, s1 - s0, r.strip * wout, fixed, per_x, per_y)});
+        }
     }
     return count;
   };
@@ -259,8 +239,7 @@ std::vector<Unit> build_units(const TileGeom& g, int K, int H, bool fixed, bool 
   if (H > 0) {
     U = (double)(H + K);
   } else {
-    // Smallest unit cost whose unit count fits one resident round (capacity waves); never
-    // shorter than 16 rows (the prologue would dominate).
+    // Smallest unit cost whose unit count fits one resident round; never below 16 rows.
     double lo = 16.0 + K, hi = (double)(g.xcell + K) * w + 1.0;
     if (plan(lo, nullptr) <= capacity) {
       hi = lo;
@@ -273,8 +252,64 @@ std::vector<Unit> build_units(const TileGeom& g, int K, int H, bool fixed, bool 
     }
     U = hi;
   }
+  std::vector<Unit> v;
   plan(U, &v);
   return v;
+}
+}  // namespace
+
+UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
+                    int64_t capacity, const bool* peer, int hb) {
+  UnitPlan P;
+  const int64_t wout = strip_out_cols(K);
+  const int64_t nstrips = (g.ycell + wout - 1) / wout;
+  hb = std::max(hb, K);
+  const bool has_peer = peer && std::any_of(peer, peer + kNumDirs, [](bool b) { return b; });
+  const bool top_bd = has_peer && (peer[kN] || peer[kNW] || peer[kNE]);
+  const bool bot_bd = has_peer && (peer[kS] || peer[kSW] || peer[kSE]);
+  std::vector<RowRange> in_r, bd_r;
+  for (int64_t s = 0; s < nstrips; ++s) {
+    const int64_t y0 = s * wout, y1 = std::min(g.ycell, y0 + wout);
+    const bool col_edge = unit_edge_flags(g, K, 0, 1, y0, fixed, true, per_y) & kEdgeCols;
+    const bool row_edge_top = unit_edge_flags(g, K, 0, 1, y0, fixed, per_x, true) & kEdgeRows;
+    const bool row_edge_bot = unit_edge_flags(g, K, g.xcell - 1, 1, y0, fixed, per_x, true) & kEdgeRows;
+    const bool lr_bd = has_peer && ((y0 - K < 0 && (peer[kW] || peer[kNW] || peer[kSW])) ||
+                                    (y1 + K > g.ycell && (peer[kE] || peer[kNE] || peer[kSE])));
+    if (lr_bd) {
+      bd_r.push_back(RowRange{s, 0, g.xcell, col_edge});
+      continue;
+    }
+    int64_t top = top_bd ? std::min<int64_t>(g.xcell, hb) : 0;
+    int64_t bot = bot_bd ? std::max<int64_t>(top, g.xcell - hb) : g.xcell;
+    if (top > 0) bd_r.push_back(RowRange{s, 0, top, true});
+    if (bot < g.xcell) bd_r.push_back(RowRange{s, bot, g.xcell, true});
+    if (!has_peer) {
+      // rows whose K-cone reaches a global edge row form short edge units
+      const int64_t he = std::min<int64_t>(g.xcell, std::max<int64_t>(hb, 2 * K));
+      int64_t t = row_edge_top ? he : 0, b = row_edge_bot ? std::max<int64_t>(t, g.xcell - he) : g.xcell;
+      if (col_edge) {
+        in_r.push_back(RowRange{s, 0, g.xcell, true});
+      } else {
+        if (t > 0) in_r.push_back(RowRange{s, 0, t, true});
+        in_r.push_back(RowRange{s, t, b, false});
+        if (b < g.xcell) in_r.push_back(RowRange{s, b, g.xcell, true});
+      }
+    } else {
+      in_r.push_back(RowRange{s, top, bot, col_edge});
+    }
+  }
+  P.interior = size_ranges(g, K, in_r, H, fixed, per_x, per_y, edge_weight, capacity);
+  // Boundary units are short (hb rows): they run first, alone, and gate the halo exchange.
+  P.boundary = size_ranges(g, K, bd_r, hb, fixed, per_x, per_y, 1.0, capacity);
+  auto edge_first = [](const Unit& a, const Unit& b) { return (a.flags != 0) > (b.flags != 0); };
+  std::stable_sort(P.interior.begin(), P.interior.end(), edge_first);
+  return P;
+}
+
+std::vector<Unit> build_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y,
+                              double edge_weight, int64_t capacity) {
+  UnitPlan p = plan_units(g, K, H, fixed, per_x, per_y, edge_weight, capacity, nullptr, 16);
+  return p.interior;
 }
 
 bool stream_k_supported(int K) {

@@ -161,3 +161,38 @@ def test_rccl_convergence_allreduce(native, gpu):
     st = eng.run(5000)
     assert st["steps_done"] == ref["steps_done"] and st["converged"] == ref["converged"]
     assert np.array_equal(eng.download(0), ref["grid"])
+
+
+@pytest.mark.parametrize("gx,gy", [(2, 1), (4, 1), (2, 2), (1, 3)])
+@pytest.mark.parametrize("concurrent", [0, 1])
+def test_overlap_pipelines(native, gpu, gx, gy, concurrent):
+    """Boundary-first (single stream) and concurrent (two streams) pipelines, with convergence."""
+    nx, ny, steps = 257, 509, 45
+    kw = dict(convergence=True, interval=9, sensitivity=1e-30)
+    for boundary in (0, 1):
+        eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=boundary, tblock=8, device=gpu,
+                            concurrent=concurrent, **kw)
+        assert eng.concurrent() == bool(concurrent)
+        st = eng.run(steps)
+        assert st["steps_done"] == steps
+        ref = oracle(native, nx, ny, steps, boundary, **kw)
+        out = np.zeros((nx, ny), np.float32)
+        for t in range(eng.num_tiles()):
+            g = eng.geom(t)
+            out[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]] = eng.download(t)
+        assert np.array_equal(out, ref["grid"]), (gx, gy, boundary, concurrent)
+
+
+def test_concurrent_auto_for_row_strips(native, gpu):
+    eng = native.Engine(2048, 2048, gridx=4, gridy=1, device=gpu)
+    assert eng.concurrent()
+
+
+@pytest.mark.parametrize("concurrent", [0, 1])
+def test_rccl_self_exchange_row_periodic(native, gpu, concurrent):
+    nx, ny, steps = 300, 700, 37
+    eng = native.Engine(nx, ny, periodic_x=True, boundary=1, device=gpu, ranks=[0], transport=native.TRANSPORT_RCCL,
+                        concurrent=concurrent)
+    eng.init_rccl(native.Engine.rccl_unique_id(), 1, 0)
+    eng.run(steps)
+    assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, 1, per=(True, False))["grid"])

@@ -110,5 +110,6 @@ def test_bench_contract_cpu_rehearsal(tmp_path, n):
         assert k in d
     assert d["n_gpus"] == n and d["steps"] == 6 and d["scaling"] == "weak"
     gx, gy = d["config"]["grid"]
+    assert d["config"]["grid_per_gpu"] == [48, 48]
     assert gx * gy == 48 * 48 * n
     assert abs(d["value"] - gx * gy * 6 / d["elapsed_s"]) / d["value"] < 1e-9
