@@ -49,6 +49,9 @@ def main() -> int:
     ap.add_argument("--layout", choices=("rows", "blocks"), default="rows")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--repeat", type=int, default=1, help="timed repetitions (best reported)")
+    ap.add_argument("--prewarm-s", type=float, default=0.3,
+                    help="seconds of untimed stencil work before the warm-up steps, so the GPU reaches its "
+                         "steady power state (the first ~10 ms after idle run at lower clocks)")
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: rehearsal of the distributed contract on the host (gloo), not a benchmark")
     a = ap.parse_args()
@@ -83,21 +86,31 @@ def main() -> int:
         if on_gpu:
             torch.cuda.synchronize()
 
-    # warm-up (untimed): also builds every lazy structure and warms caches
+    # pre-warm (untimed, time-based) then the W warm-up steps (untimed)
     run = s.run_steps
+    prewarm_steps = 0
+    if on_gpu and a.prewarm_s > 0:
+        t_end = time.perf_counter() + a.prewarm_s
+        while time.perf_counter() < t_end:
+            run(64)
+            prewarm_steps += 64
+        sync_barrier()
     if a.warmup > 0:
         run(a.warmup)
     best = None
     res = None
+    times = []
     for _ in range(max(1, a.repeat)):
         sync_barrier()
         t0 = time.perf_counter()
         res = run(a.steps)
         sync_barrier()
         dt = ctx.allreduce_max(time.perf_counter() - t0)
+        times.append(dt)
         best = dt if best is None else min(best, dt)
-    if res["steps_done"] - (a.warmup if a.warmup > 0 else 0) < 0:
-        raise SystemExit("bench: step accounting error")
+    expect = prewarm_steps + max(0, a.warmup) + a.steps * max(1, a.repeat)
+    if res["steps_done"] != expect:
+        raise SystemExit(f"bench: step accounting error ({res['steps_done']} != {expect})")
     cups = float(nx) * float(ny) * a.steps / best
     if ctx.rank == 0:
         out = {
@@ -115,6 +128,8 @@ def main() -> int:
             "compute": ("fp64 expression, bit-exact with the reference" if a.precision == "ref" else "fp32 FMA"),
             "data": "synthetic center-hot initial field (exact formula, generated on device)",
             "elapsed_s": best,
+            "repeats_s": times,
+            "prewarm_steps": prewarm_steps,
             "config": {
                 "model": "heat2d 5-point Jacobi, fixed edges" if a.boundary == "fixed" else "heat2d 5-point Jacobi, zero ghost ring",
                 "grid": [nx, ny],
@@ -122,7 +137,8 @@ def main() -> int:
                 "global_batch": nx * ny,
                 "seq_len": a.steps,
                 "parallelism": (f"rows{gx}" if a.layout == "rows" else f"blocks{gx}x{gy}") if world > 1 else "single",
-                "overlap": "concurrent" if s.engine.concurrent() else ("boundary-first" if cfg.overlap else "none"),
+                "overlap": ("none" if not s.engine.has_exchange() else
+                            "concurrent" if s.engine.concurrent() else ("boundary-first" if cfg.overlap else "off")),
                 "tblock": s.engine.halo_depth(),
                 "path": res["path"],
                 "transport": cfg.transport,

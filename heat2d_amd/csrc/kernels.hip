@@ -209,6 +209,7 @@ namespace {
 struct RowRange {
   int64_t strip, a, b;  // rows [a, b) of strip
   bool edge;            // costs `w` per row (global-edge masks)
+  bool edge_top = false, edge_bot = false;  // first / last unit is an edge unit (global edge rows)
 };
 
 // Cut every range into units of (nearly) equal cost, fitting `capacity` waves in one round.
@@ -221,17 +222,32 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<RowRan
   auto rows_for = [&](double U, bool edge) { return std::max<int64_t>(1, (int64_t)(edge ? U / w - K : U - K)); };
   auto plan = [&](double U, std::vector<Unit>* out) -> int64_t {
     int64_t count = 0;
-    for (const RowRange& r : ranges) {
-      const int64_t len = r.b - r.a;
-      if (len <= 0) continue;
-      const int64_t n = (len + rows_for(U, r.edge) - 1) / rows_for(U, r.edge);
+    auto emit = [&](int64_t strip, int64_t a, int64_t b, int64_t target) {
+      const int64_t len = b - a;
+      if (len <= 0) return;
+      const int64_t n = (len + target - 1) / target;
       count += n;
       if (out)
         for (int64_t i = 0; i < n; ++i) {
-          const int64_t s0 = r.a + len * i / n, s1 = r.a + len * (i + 1) / n;
-          out->push_back(Unit{(int)r.strip, (int)s0, (int)(s1 - s0),
-                              unit_edge_flags(g, K, s0, s1 - s0, r.strip * wout, fixed, per_x, per_y)});
+          const int64_t s0 = a + len * i / n, s1 = a + len * (i + 1) / n;
+          out->push_back(Unit{(int)strip, (int)s0, (int)(s1 - s0),
+                              unit_edge_flags(g, K, s0, s1 - s0, strip * wout, fixed, per_x, per_y)});
         }
+    };
+    for (const RowRange& r : ranges) {
+      int64_t a = r.a, b = r.b;
+      const int64_t he = rows_for(U, true);
+      if (r.edge_top && b > a) {
+        const int64_t e = std::min(b, a + he);
+        emit(r.strip, a, e, he);
+        a = e;
+      }
+      if (r.edge_bot && b > a) {
+        const int64_t e = std::max(a, b - he);
+        emit(r.strip, e, b, he);
+        b = e;
+      }
+      emit(r.strip, a, b, rows_for(U, r.edge));
     }
     return count;
   };
@@ -284,16 +300,11 @@ UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, boo
     if (top > 0) bd_r.push_back(RowRange{s, 0, top, true});
     if (bot < g.xcell) bd_r.push_back(RowRange{s, bot, g.xcell, true});
     if (!has_peer) {
-      // rows whose K-cone reaches a global edge row form short edge units
-      const int64_t he = std::min<int64_t>(g.xcell, std::max<int64_t>(hb, 2 * K));
-      int64_t t = row_edge_top ? he : 0, b = row_edge_bot ? std::max<int64_t>(t, g.xcell - he) : g.xcell;
-      if (col_edge) {
-        in_r.push_back(RowRange{s, 0, g.xcell, true});
-      } else {
-        if (t > 0) in_r.push_back(RowRange{s, 0, t, true});
-        in_r.push_back(RowRange{s, t, b, false});
-        if (b < g.xcell) in_r.push_back(RowRange{s, b, g.xcell, true});
-      }
+      // units whose K-cone reaches a global edge row are edge units (cost-balanced)
+      RowRange r{s, 0, g.xcell, col_edge};
+      r.edge_top = !col_edge && row_edge_top;
+      r.edge_bot = !col_edge && row_edge_bot;
+      in_r.push_back(r);
     } else {
       in_r.push_back(RowRange{s, top, bot, col_edge});
     }
