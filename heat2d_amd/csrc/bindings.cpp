@@ -218,7 +218,7 @@ PYBIND11_MODULE(_heat2d, m) {
       .def(py::init([](int64_t nx, int64_t ny, int gridx, int gridy, bool per_x, bool per_y, int boundary,
                        int precision, int init, double cx, double cy, int tblock, int rows_per_wave, bool convergence,
                        int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
-                       bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows) {
+                       bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s) {
              EngineOptions o;
              o.nx = nx;
              o.ny = ny;
@@ -246,6 +246,7 @@ PYBIND11_MODULE(_heat2d, m) {
              o.wave_capacity = wave_capacity;
              o.concurrent = concurrent;
              o.boundary_rows = boundary_rows;
+             o.watchdog_s = watchdog_s;
              return new Engine(o);
            }),
            py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
@@ -255,7 +256,8 @@ PYBIND11_MODULE(_heat2d, m) {
            py::arg("interval") = 20, py::arg("sensitivity") = 0.1, py::arg("device") = 0,
            py::arg("ranks") = std::vector<int>{}, py::arg("transport") = (int)kTransportAuto,
            py::arg("overlap") = true, py::arg("small_grid_lds") = true, py::arg("naive") = false,
-           py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0, py::arg("concurrent") = -1, py::arg("boundary_rows") = 16)
+           py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0, py::arg("concurrent") = -1, py::arg("boundary_rows") = 16,
+           py::arg("watchdog_s") = 900.0)
       .def("num_tiles", &Engine::num_tiles)
       .def("tile_rank", &Engine::tile_rank)
       .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })

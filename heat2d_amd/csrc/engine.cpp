@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 #define H2D_NCCL_CHECK(call)                                                                             \
   do {                                                                                                   \
@@ -460,13 +461,41 @@ double Engine::local_residual() {
   return s;
 }
 
+void Engine::wait_event(hipEvent_t ev) {
+  // Failure detection: with a communicator, poll the event and RCCL's asynchronous error
+  // state instead of blocking, and abort the communicator after `watchdog_s` without
+  // completion (a dead peer would otherwise hang the rank forever).
+  if (!rccl_comm_) {
+    H2D_HIP_CHECK(hipEventSynchronize(ev));
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 0;; ++spin) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) H2D_HIP_CHECK(e);
+    ncclResult_t async = ncclSuccess;
+    ncclCommGetAsyncError((ncclComm_t)rccl_comm_, &async);
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (async != ncclSuccess || (opt_.watchdog_s > 0 && el > opt_.watchdog_s)) {
+      const std::string why = async != ncclSuccess ? std::string("RCCL async error: ") + ncclGetErrorString(async)
+                                                   : "watchdog: no progress for " + std::to_string(el) + " s";
+      ncclCommAbort((ncclComm_t)rccl_comm_);
+      rccl_comm_ = nullptr;
+      throw std::runtime_error("[rank " + std::to_string(rccl_rank_) + "] " + why);
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 double Engine::finish_residual() {
   if (on_gpu() && rccl_comm_) {
     // Local sum over tiles (one tile under RCCL) -> all-reduce across ranks on the compute stream.
     H2D_NCCL_CHECK(ncclAllReduce(d_resid_, d_resid_ + tiles_.size(), 1, ncclDouble, ncclSum, (ncclComm_t)rccl_comm_,
                                  compute_));
     H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_ + tiles_.size(), sizeof(double), hipMemcpyDeviceToHost, compute_));
-    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
+    wait_event(ev_ready_);
     return h_resid_[0];
   }
   return local_residual();
@@ -477,6 +506,16 @@ void Engine::rollback() {
 }
 
 RunStats Engine::run(int64_t steps) {
+  try {
+    return run_impl(steps);
+  } catch (const std::exception& e) {
+    const std::string m = e.what();
+    if (m.rfind("[rank ", 0) == 0) throw;
+    throw std::runtime_error("[rank " + std::to_string(tiles_.empty() ? 0 : tiles_[0].rank) + "] " + m);
+  }
+}
+
+RunStats Engine::run_impl(int64_t steps) {
   if (transport_ == kTransportExternal && has_exchange_)
     throw std::runtime_error("external transport: drive the loop from the caller");
   if (transport_ == kTransportRccl && has_exchange_ && !rccl_comm_)
@@ -667,7 +706,7 @@ RunStats Engine::run(int64_t steps) {
     }
     H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
   }
-  H2D_HIP_CHECK(hipEventSynchronize(ev_t1_));
+  wait_event(ev_t1_);
   float ms = 0.0f;
   H2D_HIP_CHECK(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
   st.device_ms = ms;

@@ -52,6 +52,7 @@ struct EngineOptions {
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   int boundary_rows = 16;     // rows per halo-dependent work unit (overlap mode)
   int concurrent = -1;        // boundary units on a second stream: -1 auto, 0 never, 1 always
+  double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool convergence = false;
   int64_t interval = 20;
   double sensitivity = 0.1;
@@ -146,6 +147,8 @@ class Engine {
   void reduce_tile_residual(int t, int K);
   void do_exchange_async(int K);  // enqueue on comm stream
   double finish_residual();       // reduce + (rccl) all-reduce, host sync
+  void wait_event(hipEvent_t ev);  // blocking wait with RCCL error polling + watchdog
+  RunStats run_impl(int64_t steps);
   CopyDesc* local_descs(int K, int& n, int64_t& maxe);
   void check_tile(int t) const;
 

@@ -81,19 +81,22 @@ class Solver:
         else:
             self.device = -1
         self.transport = transport
-        self.engine = n.Engine(
-            cfg.nx, cfg.ny, gridx=self.gridx, gridy=self.gridy, periodic_x=self.model.periodic_x,
-            periodic_y=self.model.periodic_y, boundary=self.model.boundary_id(), precision=self.model.precision_id(),
-            init=self.model.init_id(), cx=self.model.cx, cy=self.model.cy, tblock=cfg.tblock,
-            rows_per_wave=cfg.rows_per_wave, convergence=cfg.convergence, interval=cfg.interval,
-            sensitivity=cfg.sensitivity, device=self.device, ranks=ranks, transport=transport,
-            overlap=cfg.overlap, small_grid_lds=cfg.small_grid, naive=cfg.naive)
+        self.engine = self._make_engine(transport, ranks)
         self.exchanger = None
         if transport == n.TRANSPORT_RCCL and self.engine.has_exchange():
-            uid = n.Engine.rccl_unique_id() if self.ctx.rank == 0 else None
-            uid = self.ctx.broadcast_bytes(uid)
-            self.engine.init_rccl(uid, world, self.ctx.rank)
-        elif transport == n.TRANSPORT_EXTERNAL and self.engine.has_exchange():
+            ok = 1
+            try:
+                uid = n.Engine.rccl_unique_id() if self.ctx.rank == 0 else None
+                uid = self.ctx.broadcast_bytes(uid)
+                self.engine.init_rccl(uid, world, self.ctx.rank)
+            except Exception as e:  # pragma: no cover - needs a broken multi-GPU setup
+                ok = 0
+                print(f"[rank {self.ctx.rank}] native RCCL init failed: {e}", flush=True)
+            if self.ctx.allreduce_sum(ok) < world:
+                # every rank falls back together to torch.distributed p2p (nccl backend = RCCL)
+                transport = self.transport = n.TRANSPORT_EXTERNAL
+                self.engine = self._make_engine(transport, ranks)
+        if transport == n.TRANSPORT_EXTERNAL and self.engine.has_exchange():
             dev = torch.device("cuda", self.device) if self.on_gpu else torch.device("cpu")
             group = self.ctx.get_nccl_group() if self.on_gpu else None
             self.exchanger = TorchHaloExchanger(self.engine, 0, dev, group)
@@ -104,6 +107,16 @@ class Solver:
                 self.engine.upload(t, full[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]])
             self.engine.set_steps_done(cfg.start_step)
         self.reporter = Reporter(cfg.report, enabled=(self.ctx.rank == 0 and not cfg.quiet))
+
+    def _make_engine(self, transport: int, ranks):
+        cfg, n = self.cfg, native()
+        return n.Engine(
+            cfg.nx, cfg.ny, gridx=self.gridx, gridy=self.gridy, periodic_x=self.model.periodic_x,
+            periodic_y=self.model.periodic_y, boundary=self.model.boundary_id(), precision=self.model.precision_id(),
+            init=self.model.init_id(), cx=self.model.cx, cy=self.model.cy, tblock=cfg.tblock,
+            rows_per_wave=cfg.rows_per_wave, convergence=cfg.convergence, interval=cfg.interval,
+            sensitivity=cfg.sensitivity, device=self.device, ranks=ranks, transport=transport,
+            overlap=cfg.overlap, small_grid_lds=cfg.small_grid, naive=cfg.naive)
 
     # ---- data access -------------------------------------------------------------------
     def tiles(self):
