@@ -48,6 +48,7 @@ class Config:
     overlap: bool = True
     small_grid: bool = True
     naive: bool = False
+    tune: bool = False  # autotune K / rows-per-wave on scratch engines before the run (single GPU)
     json: bool = False
     quiet: bool = False
     load: Optional[str] = None  # resume: raw NX×NY fp32 grid (extension)
@@ -125,6 +126,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-overlap", action="store_true", help="do not overlap halo exchange with interior compute")
     p.add_argument("--no-small-grid", action="store_true", help="disable the whole-grid LDS solver")
     p.add_argument("--naive", action="store_true", help="validation kernel: one thread per cell, one step per launch")
+    p.add_argument("--tune", action="store_true", help="autotune the temporal block / unit size before the run")
     p.add_argument("--json", action="store_true", help="print a JSON metrics line")
     p.add_argument("--quiet", action="store_true", help="no banners")
     p.add_argument("--load", default=None, help="resume from a raw NX×NY fp32 grid (extension)")
@@ -169,6 +171,7 @@ def config_from_args(argv: Optional[Sequence[str]] = None) -> Config:
         overlap=not a.no_overlap,
         small_grid=not a.no_small_grid,
         naive=a.naive,
+        tune=a.tune,
         json=a.json,
         quiet=a.quiet,
         load=a.load,

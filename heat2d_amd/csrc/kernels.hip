@@ -79,9 +79,12 @@ __global__ __launch_bounds__(256) void tile_residual_kernel(TileGeom g, const fl
 // Small-grid resident solver: one 1024-thread workgroup keeps the whole grid in LDS and runs
 // every time step (and the convergence test) without returning to the host.  Replaces
 // ~2 launches/step of the reference CUDA program (grad1612_cuda_heat.cu:82-85) for grids up
-// to 40960 cells, where a GPU is otherwise launch-latency bound.
+// to 20480 cells, where a GPU is otherwise launch-latency bound.
+// The LDS image carries a one-cell ring (zero, or the periodic wrap refreshed every step), so
+// neighbour reads are fixed offsets; new values live in registers between the two barriers.
 // ------------------------------------------------------------------------------------------
-constexpr int kLdsCells = 20480;  // 80 KiB of fp32: 160x128 (the largest grid the reference CUDA table runs in 71 us/step)
+constexpr int kLdsCells = 20480;         // interior cells (160x128, the reference CUDA table's size)
+constexpr int kLdsImage = 40960 - 256;   // ring-padded image, floats
 constexpr int kLdsThreads = 1024;
 constexpr int kLdsPerThread = kLdsCells / kLdsThreads;
 
@@ -91,42 +94,27 @@ __global__ __launch_bounds__(1024) void lds_solver_kernel(const float* __restric
                                                            long long steps, Coef k, int fixed, int per_x, int per_y,
                                                            int interval, double sens, long long* steps_done,
                                                            double* residual) {
-  __shared__ float u[kLdsCells];
+  __shared__ float u[kLdsImage];
   __shared__ double red[16];
   __shared__ int stop_flag;
   const int tid = threadIdx.x;
+  const int W = NY + 2;
   const int ncell = NX * NY;
-  for (int e = tid; e < ncell; e += kLdsThreads) u[e] = in[(int64_t)(e / NY) * in_pitch + (e % NY)];
-  const int di = kLdsThreads / NY, dj = kLdsThreads % NY;
-  const int i0 = tid / NY, j0 = tid % NY;
-  double last_res = -1.0;
-  long long done = 0;
+  const int nimg = (NX + 2) * W;
+  for (int e = tid; e < nimg; e += kLdsThreads) u[e] = 0.0f;
   __syncthreads();
-  for (long long step = 1; step <= steps; ++step) {
-    float nv[kLdsPerThread];
-    double racc = 0.0;
-    int i = i0, j = j0;
+  for (int e = tid; e < ncell; e += kLdsThreads) u[(e / NY + 1) * W + (e % NY) + 1] = in[(int64_t)(e / NY) * in_pitch + (e % NY)];
+  // per-thread cells: LDS offsets and the fixed-edge hold mask
+  int L[kLdsPerThread];
+  unsigned hold = 0;
+  {
+    int i = tid / NY, j = tid % NY;
+    const int di = kLdsThreads / NY, dj = kLdsThreads % NY;
 #pragma unroll
     for (int q = 0; q < kLdsPerThread; ++q) {
-      const int idx = tid + q * kLdsThreads;
-      if (idx < ncell) {
-        const int m = max(dim_mode(i, NX, per_x != 0, fixed != 0), dim_mode(j, NY, per_y != 0, fixed != 0));
-        const float cc = u[idx];
-        float v;
-        if (m == 2) {
-          v = 0.0f;
-        } else if (m == 1) {
-          v = cc;
-        } else {
-          const float nn = i > 0 ? u[idx - NY] : (per_x ? u[idx + (NX - 1) * NY] : 0.0f);
-          const float ss = i < NX - 1 ? u[idx + NY] : (per_x ? u[idx - (NX - 1) * NY] : 0.0f);
-          const float ww = j > 0 ? u[idx - 1] : (per_y ? u[idx + NY - 1] : 0.0f);
-          const float ee = j < NY - 1 ? u[idx + 1] : (per_y ? u[idx - (NY - 1)] : 0.0f);
-          v = cell<F32>(cc, nn, ss, ww, ee, k);
-        }
-        nv[q] = v;
-        racc += sq_diff(v, cc);
-      }
+      L[q] = (i + 1) * W + (j + 1);
+      const bool h = fixed && ((!per_x && (i == 0 || i == NX - 1)) || (!per_y && (j == 0 || j == NY - 1)));
+      hold |= (h ? 1u : 0u) << q;
       j += dj;
       i += di;
       if (j >= NY) {
@@ -134,7 +122,39 @@ __global__ __launch_bounds__(1024) void lds_solver_kernel(const float* __restric
         i += 1;
       }
     }
+  }
+  double last_res = -1.0;
+  long long done = 0;
+  __syncthreads();
+  for (long long step = 1; step <= steps; ++step) {
+    if (per_x || per_y) {  // refresh the periodic ring
+      if (per_x)
+        for (int j = tid; j < NY; j += kLdsThreads) {
+          u[j + 1] = u[NX * W + j + 1];
+          u[(NX + 1) * W + j + 1] = u[W + j + 1];
+        }
+      __syncthreads();
+      if (per_y)
+        for (int i = tid; i < NX + 2; i += kLdsThreads) {
+          u[i * W] = u[i * W + NY];
+          u[i * W + NY + 1] = u[i * W + 1];
+        }
+      __syncthreads();
+    }
     const bool check = interval > 0 && (step % interval) == 0;
+    float nv[kLdsPerThread];
+    double racc = 0.0;
+#pragma unroll
+    for (int q = 0; q < kLdsPerThread; ++q) {
+      if (tid + q * kLdsThreads < ncell) {
+        const int c = L[q];
+        const float cc = u[c];
+        float v = cell<F32>(cc, u[c - W], u[c + W], u[c - 1], u[c + 1], k);
+        v = ((hold >> q) & 1u) ? cc : v;
+        nv[q] = v;
+        if (check) racc += sq_diff(v, cc);
+      }
+    }
     if (check) {  // block-uniform
       racc = wave_sum(racc);
       if ((tid & 63) == 0) red[tid >> 6] = racc;
@@ -151,14 +171,12 @@ __global__ __launch_bounds__(1024) void lds_solver_kernel(const float* __restric
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kLdsPerThread; ++q) {
-      const int idx = tid + q * kLdsThreads;
-      if (idx < ncell) u[idx] = nv[q];
-    }
+    for (int q = 0; q < kLdsPerThread; ++q)
+      if (tid + q * kLdsThreads < ncell) u[L[q]] = nv[q];
     __syncthreads();
     done = step;
   }
-  for (int e = tid; e < ncell; e += kLdsThreads) out[(int64_t)(e / NY) * out_pitch + (e % NY)] = u[e];
+  for (int e = tid; e < ncell; e += kLdsThreads) out[(int64_t)(e / NY) * out_pitch + (e % NY)] = u[(e / NY + 1) * W + (e % NY) + 1];
   if (tid == 0) {
     *steps_done = done;
     *residual = last_res;
@@ -255,8 +273,8 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<RowRan
   if (H > 0) {
     U = (double)(H + K);
   } else {
-    // Smallest unit cost whose unit count fits one resident round; never below 16 rows.
-    double lo = 16.0 + K, hi = (double)(g.xcell + K) * w + 1.0;
+    // Smallest unit cost whose unit count fits one resident round; never below 8 rows.
+    double lo = 8.0 + K, hi = (double)(g.xcell + K) * w + 1.0;
     if (plan(lo, nullptr) <= capacity) {
       hi = lo;
     } else {
@@ -383,7 +401,9 @@ void launch_tile_residual(const TileGeom& g, const float* a, const float* b, dou
   H2D_HIP_CHECK(hipGetLastError());
 }
 
-bool lds_solver_fits(int64_t NX, int64_t NY) { return NX >= 1 && NY >= 1 && NX * NY <= kLdsCells; }
+bool lds_solver_fits(int64_t NX, int64_t NY) {
+  return NX >= 1 && NY >= 1 && NX * NY <= kLdsCells && (NX + 2) * (NY + 2) <= kLdsImage;
+}
 
 void launch_lds_solver(const float* in, int64_t in_pitch, float* out, int64_t out_pitch, int64_t NX, int64_t NY,
                        int64_t steps, int precision, int boundary, double cx, double cy, bool per_x, bool per_y,

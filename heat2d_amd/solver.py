@@ -49,6 +49,41 @@ class RunResult:
     extra: dict = field(default_factory=dict)
 
 
+def autotune(cfg: Config, model, device: int, candidates_k=(2, 4, 8), candidates_h=(0, 4, 8, 16, 32),
+             trial_steps: int = 0) -> dict:
+    """Pick the temporal-block depth K and rows per wave H for a single-tile GPU run by
+    timing each candidate on a scratch engine (the real field is untouched).  Small and
+    medium grids are latency-bound and prefer short units; large grids keep the defaults."""
+    n = native()
+    cells = cfg.nx * cfg.ny
+    steps = trial_steps or max(32, min(256, int(2e8 // max(1, cells))))
+    table = []
+    best = None
+    if n.lds_solver_fits(cfg.nx, cfg.ny) and cfg.small_grid:
+        e = n.Engine(cfg.nx, cfg.ny, boundary=model.boundary_id(), precision=model.precision_id(),
+                     init=model.init_id(), cx=model.cx, cy=model.cy, device=device, small_grid_lds=True)
+        e.run(steps)
+        t = min(e.run(steps)["device_ms"] for _ in range(2)) / steps
+        table.append(("lds", 0, t))
+        best = ("lds", 0, t)
+    for K in candidates_k:
+        for H in candidates_h:
+            e = n.Engine(cfg.nx, cfg.ny, boundary=model.boundary_id(), precision=model.precision_id(),
+                         init=model.init_id(), cx=model.cx, cy=model.cy, tblock=K, rows_per_wave=H, device=device,
+                         small_grid_lds=False)
+            e.run(steps)  # warm
+            t = min(e.run(steps)["device_ms"] for _ in range(2)) / steps
+            table.append((K, H, t))
+            if best is None or t < best[2]:
+                best = (K, H, t)
+            del e
+    if best[0] == "lds":
+        return {"tblock": cfg.tblock, "rows_per_wave": 0, "small_grid": True, "us_per_step": best[2] * 1e3,
+                "table": table}
+    return {"tblock": best[0], "rows_per_wave": best[1], "small_grid": False, "us_per_step": best[2] * 1e3,
+            "table": table}
+
+
 class Solver:
     def __init__(self, cfg: Config, ctx: Optional[DistContext] = None, device_ordinal: Optional[int] = None):
         self.cfg = cfg
@@ -81,6 +116,11 @@ class Solver:
         else:
             self.device = -1
         self.transport = transport
+        self.tuned = None
+        if cfg.tune and self.on_gpu and world == 1 and self.nranks == 1:
+            self.tuned = autotune(cfg, self.model, self.device)
+            cfg.tblock, cfg.rows_per_wave = self.tuned["tblock"], self.tuned["rows_per_wave"]
+            cfg.small_grid = self.tuned["small_grid"]
         self.engine = self._make_engine(transport, ranks)
         self.exchanger = None
         if transport == n.TRANSPORT_RCCL and self.engine.has_exchange():
