@@ -1,0 +1,213 @@
+// heat2d — the native command-line program (one process: one GPU with all GRIDX×GRIDY tiles
+// as local tiles, or the CPU).  Same flags, presets, banners and output files as
+// `python -m heat2d_amd` (multi-GPU runs go through torch.distributed + RCCL in Python).
+//
+// Replaces the compile-time #define knobs of the reference programs
+// (grad1612_mpi_heat.c:5-21, mpi_heat2Dn.c:29-44, grad1612_hybrid_heat.c:6-24,
+// grad1612_cuda_heat.cu:6-13) with runtime flags; banners follow C-IO-4.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <sys/stat.h>
+#include <vector>
+
+#include "cpu_reference.h"
+#include "decomposition.h"
+#include "engine.h"
+#include "io.h"
+
+using namespace h2d;
+
+namespace {
+
+struct Preset {
+  int64_t nx, ny, steps;
+  int gridx, gridy;
+  int boundary;
+  double cx;
+  bool convergence;
+  std::string report, text;
+  bool binary;
+  bool strips;
+};
+
+const std::map<std::string, Preset>& presets() {
+  static const std::map<std::string, Preset> p = {
+      {"heat2d", {10, 10, 100, 1, 1, kFixed, kCxDouble, false, "grad", "grad", true, false}},
+      {"heat2dn", {10, 10, 100, 1, 1, kFixed, kCxFloat, false, "heat2dn", "heat2dn", false, true}},
+      {"grad_mpi", {10, 10, 100, 2, 2, kGhostZero, kCxDouble, false, "grad", "grad", true, false}},
+      {"grad_hybrid", {10, 10, 100, 1, 1, kGhostZero, kCxDouble, true, "hybrid", "grad", true, false}},
+      {"cuda", {640, 1024, 10000, 1, 1, kFixed, kCxDouble, false, "cuda", "none", false, false}},
+  };
+  return p;
+}
+
+[[noreturn]] void usage(const char* msg) {
+  if (msg) std::fprintf(stderr, "heat2d: %s\n", msg);
+  std::fprintf(stderr,
+               "usage: heat2d [--preset heat2d|heat2dn|grad_mpi|grad_hybrid|cuda] [--nx N] [--ny N] [--steps N]\n"
+               "              [--gridx N] [--gridy N] [--convergence 0|1] [--interval N] [--sensitivity X]\n"
+               "              [--cx X] [--cy X] [--boundary fixed|ghost-zero] [--init exact|ref-int32|zero]\n"
+               "              [--precision ref|fp32] [--periodic none|x|y|xy] [--output auto|text|binary|both|none]\n"
+               "              [--outdir DIR] [--device gpu|cpu] [--tblock K] [--rows-per-wave H] [--no-overlap]\n"
+               "              [--numthreads N] [--debug 0|1] [--json] [--quiet]\n");
+  std::exit(2);
+}
+
+void write_outputs(Engine& e, const std::string& outdir, const char* which, int64_t NX, int64_t NY, bool binary,
+                   bool text, int style) {
+  if (!binary && !text) return;
+  ::mkdir(outdir.c_str(), 0755);
+  const std::string bin = outdir + "/" + which + "_binary.dat";
+  const std::string tmp = binary ? bin : outdir + "/." + which + "_binary.tmp";
+  binary_create(tmp, NX, NY);
+  for (int t = 0; t < e.num_tiles(); ++t) {
+    const TileGeom g = e.geom(t);
+    const std::vector<float> b = e.download(t);
+    binary_write_tile(tmp, NX, NY, g.gx0, g.gy0, g.xcell, g.ycell, b.data());
+  }
+  if (text) binary_to_text(tmp, outdir + "/" + which + ".dat", NX, NY, style);
+  if (!binary) std::remove(tmp.c_str());
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::map<std::string, std::string> a;
+  for (int i = 1; i < argc; ++i) {
+    std::string k = argv[i];
+    if (k.rfind("--", 0) != 0) usage(("unexpected argument " + k).c_str());
+    k = k.substr(2);
+    if (k == "no-overlap" || k == "json" || k == "quiet" || k == "help") {
+      a[k] = "1";
+      continue;
+    }
+    if (i + 1 >= argc) usage(("missing value for --" + k).c_str());
+    a[k] = argv[++i];
+  }
+  if (a.count("help")) usage(nullptr);
+  const std::string pname = a.count("preset") ? a["preset"] : "heat2d";
+  if (!presets().count(pname)) usage("unknown preset");
+  const Preset P = presets().at(pname);
+  auto geti = [&](const char* k, int64_t d) { return a.count(k) ? std::atoll(a[k].c_str()) : d; };
+  auto getd = [&](const char* k, double d) { return a.count(k) ? std::atof(a[k].c_str()) : d; };
+
+  EngineOptions o;
+  o.nx = geti("nx", P.nx);
+  o.ny = geti("ny", P.ny);
+  const int64_t steps = geti("steps", P.steps);
+  o.gridx = (int)geti("gridx", P.gridx);
+  o.gridy = (int)geti("gridy", P.gridy);
+  if (o.gridx < 1 || o.gridy < 1) usage("gridx/gridy must be >= 1 in the single-process program");
+  if (P.strips && !a.count("gridy")) o.gridy = 1;
+  o.convergence = geti("convergence", P.convergence ? 1 : 0) != 0;
+  o.interval = geti("interval", 20);
+  o.sensitivity = getd("sensitivity", 0.1);
+  o.cx = getd("cx", P.cx);
+  o.cy = getd("cy", P.cx);
+  o.boundary = P.boundary;
+  if (a.count("boundary")) o.boundary = a["boundary"] == "fixed" ? kFixed : kGhostZero;
+  const std::string init = a.count("init") ? a["init"] : "exact";
+  o.init = init == "exact" ? kInitExact : init == "ref-int32" ? kInitInt32 : kInitZero;
+  o.precision = (a.count("precision") && a["precision"] == "fp32") ? kFp32 : kRef;
+  const std::string per = a.count("periodic") ? a["periodic"] : "none";
+  o.periodic_x = per.find('x') != std::string::npos;
+  o.periodic_y = per.find('y') != std::string::npos;
+  o.tblock = (int)geti("tblock", 8);
+  o.rows_per_wave = (int)geti("rows-per-wave", 0);
+  o.overlap = !a.count("no-overlap");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  const std::string dev = a.count("device") ? a["device"] : (ndev > 0 ? "gpu" : "cpu");
+  if (dev == "gpu" && ndev == 0) usage("--device gpu but no HIP device is visible");
+  o.device = dev == "gpu" ? 0 : -1;
+  o.transport = kTransportLocal;
+  const bool quiet = a.count("quiet") > 0;
+  std::string output = a.count("output") ? a["output"] : "auto";
+  if (output == "auto") {
+    const bool t = P.text != "none";
+    output = t && P.binary ? "both" : t ? "text" : P.binary ? "binary" : "none";
+  }
+  const bool wbin = output == "binary" || output == "both";
+  const bool wtxt = output == "text" || output == "both";
+  const std::string outdir = a.count("outdir") ? a["outdir"] : ".";
+  const int tstyle = P.text == "heat2dn" ? kTextHeat2dn : kTextGrad;
+  const std::string rep = P.report;
+
+  try {
+    Engine e(o);
+    const Decomposition& d = e.decomposition();
+    const int nprocs = d.nranks();
+    if (!quiet) {
+      if (rep == "grad" || rep == "hybrid") {
+        if (rep == "grad") std::printf("Starting with %d processes\n", nprocs);
+        else std::printf("Starting with %d processes and %d threads\n", nprocs, (int)geti("numthreads", 4));
+        std::printf("Problem size:%lldx%lld\nEach process will take: %lldx%lld\nAmount of iterations: %lld\n",
+                    (long long)o.nx, (long long)o.ny, (long long)d.xcount[0], (long long)d.ycount[0],
+                    (long long)steps);
+        if (o.convergence) std::printf("Check for convergence every %lld iterations\n", (long long)o.interval);
+      } else if (rep == "heat2dn") {
+        std::printf("Starting mpi_heat2D with %d worker tasks.\n", nprocs);
+        std::printf("Grid size: X= %lld  Y= %lld  Time steps= %lld\n", (long long)o.nx, (long long)o.ny,
+                    (long long)steps);
+        std::printf("Initializing grid and writing initial.dat file...\n");
+        for (int i = 0; i < d.gridx; ++i)
+          std::printf("Sent to task %d: rows= %lld offset= %lld left= %d right= %d\n", i + 1,
+                      (long long)d.xcount[i], (long long)d.xstart[i], i == 0 ? 0 : i, i == d.gridx - 1 ? 0 : i + 2);
+      } else if (rep == "cuda") {
+        std::printf("Problem size: %lldx%lld\nAmount of iterations: %lld\n", (long long)o.nx, (long long)o.ny,
+                    (long long)steps);
+      }
+      if (geti("debug", 0)) {
+        for (int t = 0; t < e.num_tiles(); ++t) {
+          const int r = e.tile_rank(t);
+          std::printf("I am %d and my neighbors are North=%d, South=%d, East=%d, West=%d (Running on %s)\n", r,
+                      d.neighbor(r, kN), d.neighbor(r, kS), d.neighbor(r, kE), d.neighbor(r, kW),
+                      dev == "gpu" ? "gpu0" : "cpu");
+        }
+      }
+    }
+    if (output != "none") {
+      if (!quiet && (rep == "grad" || rep == "hybrid")) std::printf("Writing initial.dat ...\n");
+      write_outputs(e, outdir, "initial", o.nx, o.ny, wbin, wtxt, tstyle);
+    }
+    if (!quiet && rep == "heat2dn")
+      for (int i = 0; i < d.gridx; ++i) std::printf("Task %d received work. Beginning time steps...\n", i + 1);
+    std::fflush(stdout);
+    e.synchronize();
+    const auto t0 = std::chrono::steady_clock::now();
+    const RunStats st = e.run(steps);
+    e.synchronize();
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!quiet) {
+      if (rep == "grad" || rep == "hybrid") {
+        std::printf("Exiting after %lld iterations\nElapsed time: %e sec\n", (long long)st.steps_done, el);
+        if (output != "none") std::printf("Writing final.dat ...\n");
+      } else if (rep == "heat2dn") {
+        std::printf("Elapsed time: %e sec\n", el);
+        std::printf("Writing final.dat file and generating graph...\n");
+        std::printf("Click on MORE button to view initial/final states.\n");
+        std::printf("Click on EXIT button to quit program.\n");
+      } else if (rep == "cuda") {
+        std::printf("Elapsed time: %e sec\n", el);
+      }
+    }
+    if (output != "none") write_outputs(e, outdir, "final", o.nx, o.ny, wbin, wtxt, tstyle);
+    if (a.count("json")) {
+      const double cups = el > 0 ? (double)o.nx * (double)o.ny * (double)st.steps_done / el : 0.0;
+      std::printf("{\"grid\": [%lld, %lld], \"steps\": %lld, \"elapsed_s\": %.9g, \"cell_updates_per_s\": %.9g, "
+                  "\"path\": \"%s\", \"device\": \"%s\", \"tiles\": %d, \"converged\": %s, \"chunks\": %lld}\n",
+                  (long long)o.nx, (long long)o.ny, (long long)st.steps_done, el, cups, st.path.c_str(), dev.c_str(),
+                  e.num_tiles(), st.converged ? "true" : "false", (long long)st.chunks);
+    }
+  } catch (const std::exception& ex) {
+    std::fprintf(stderr, "heat2d: error: %s\n", ex.what());
+    return 1;
+  }
+  return 0;
+}

@@ -258,7 +258,7 @@ class Solver:
         if c.save:
             self.save(c.save)
         if c.json and self.ctx.rank == 0:
-            rep.json_line(metrics(c.nx, c.ny, res.steps_done, res.elapsed_s, ranks=self.nranks,
+            Reporter(c.report, enabled=True).json_line(metrics(c.nx, c.ny, res.steps_done, res.elapsed_s, ranks=self.nranks,
                                   tiles=res.ntiles, path=res.path, converged=res.converged,
                                   residual=res.residual, device="gpu" if self.on_gpu else "cpu",
                                   precision=c.precision, boundary=c.boundary, tblock=self.engine.halo_depth(),
