@@ -71,6 +71,8 @@ py::dict stats_dict(const RunStats& s) {
   d["chunks"] = s.chunks;
   d["exchanges"] = s.exchanges;
   d["path"] = s.path;
+  d["phase_ms"] = s.phase_ms;
+  d["phase_count"] = s.phase_count;
   return d;
 }
 
@@ -218,7 +220,7 @@ PYBIND11_MODULE(_heat2d, m) {
       .def(py::init([](int64_t nx, int64_t ny, int gridx, int gridy, bool per_x, bool per_y, int boundary,
                        int precision, int init, double cx, double cy, int tblock, int rows_per_wave, bool convergence,
                        int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
-                       bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s) {
+                       bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s, bool trace, bool poison) {
              EngineOptions o;
              o.nx = nx;
              o.ny = ny;
@@ -247,6 +249,8 @@ PYBIND11_MODULE(_heat2d, m) {
              o.concurrent = concurrent;
              o.boundary_rows = boundary_rows;
              o.watchdog_s = watchdog_s;
+             o.trace = trace;
+             o.poison = poison;
              return new Engine(o);
            }),
            py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
@@ -257,7 +261,7 @@ PYBIND11_MODULE(_heat2d, m) {
            py::arg("ranks") = std::vector<int>{}, py::arg("transport") = (int)kTransportAuto,
            py::arg("overlap") = true, py::arg("small_grid_lds") = true, py::arg("naive") = false,
            py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0, py::arg("concurrent") = -1, py::arg("boundary_rows") = 16,
-           py::arg("watchdog_s") = 900.0)
+           py::arg("watchdog_s") = 900.0, py::arg("trace") = false, py::arg("poison") = false)
       .def("num_tiles", &Engine::num_tiles)
       .def("tile_rank", &Engine::tile_rank)
       .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })

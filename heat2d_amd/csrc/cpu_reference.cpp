@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <limits>
 #include <stdexcept>
 
 namespace h2d {
@@ -124,6 +125,14 @@ double cpu_tile_advance(const TileGeom& g, const Physics& ph, const float* src, 
     in = out;
   }
   return rsum;
+}
+
+void cpu_tile_poison(const TileGeom& g, float* base, bool fixed, bool per_x, bool per_y) {
+  const float nan = std::numeric_limits<float>::quiet_NaN();
+  for (int64_t e = 0; e < g.elems(); ++e) {
+    const int64_t i = e / g.pitch - g.G, j = e % g.pitch - g.PL;
+    if (poisonable(g, i, j, fixed, per_x, per_y)) base[e] = nan;
+  }
 }
 
 void cpu_copy_rects(const std::vector<CopyDesc>& descs) {

@@ -46,6 +46,9 @@ double cpu_tile_advance(const TileGeom& g, const Physics& ph, const float* src, 
 // Initialise a tile's storage: owned cells from the init formula, everything else zero.
 void cpu_tile_init(const TileGeom& g, float* base, int init);
 
+// Debug canary: NaN into every storage cell no valid update may read (see poisonable()).
+void cpu_tile_poison(const TileGeom& g, float* base, bool fixed, bool per_x, bool per_y);
+
 // Strided rectangle copies (pack / unpack / local halo copies).
 void cpu_copy_rects(const std::vector<CopyDesc>& descs);
 

@@ -3,6 +3,8 @@
 
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -27,7 +29,57 @@ T* dmalloc(size_t n) {
   H2D_HIP_CHECK(hipMalloc(&p, n * sizeof(T)));
   return p;
 }
+// roctx markers (optional; resolved at run time so the library is not a link dependency).
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    void* h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
+    if (h) {
+      push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+      pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    }
+  }
+};
+Roctx& roctx() {
+  static Roctx r;
+  return r;
+}
 }  // namespace
+
+void Engine::trace_begin(const char* phase, hipStream_t s) {
+  if (!opt_.trace || !on_gpu()) return;
+  if (roctx().push) roctx().push(phase);
+  hipEvent_t a;
+  H2D_HIP_CHECK(hipEventCreate(&a));
+  H2D_HIP_CHECK(hipEventRecord(a, s));
+  open_[phase] = a;
+}
+
+void Engine::trace_end(const char* phase, hipStream_t s) {
+  if (!opt_.trace || !on_gpu()) return;
+  if (roctx().pop) roctx().pop();
+  hipEvent_t b;
+  H2D_HIP_CHECK(hipEventCreate(&b));
+  H2D_HIP_CHECK(hipEventRecord(b, s));
+  spans_.push_back({phase, open_.at(phase), b});
+  open_.erase(phase);
+}
+
+void Engine::trace_collect(RunStats& st) {
+  if (!opt_.trace || !on_gpu()) return;
+  for (auto& sp : spans_) {
+    H2D_HIP_CHECK(hipEventSynchronize(sp.b));
+    float ms = 0.0f;
+    H2D_HIP_CHECK(hipEventElapsedTime(&ms, sp.a, sp.b));
+    st.phase_ms[sp.phase] += ms;
+    st.phase_count[sp.phase] += 1;
+    hipEventDestroy(sp.a);
+    hipEventDestroy(sp.b);
+  }
+  spans_.clear();
+}
 
 Engine::Engine(const EngineOptions& o) : opt_(o) {
   dec_ = Decomposition(o.nx, o.ny, o.gridx, o.gridy, o.periodic_x, o.periodic_y);
@@ -86,6 +138,9 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
         H2D_HIP_CHECK(hipMemsetAsync(t.buf[b], 0, n * sizeof(float), compute_));
       }
       launch_init(t.g, t.buf[0], o.init, compute_);
+      if (o.poison)
+        for (int b = 0; b < 2; ++b)
+          launch_poison(t.g, t.buf[b], o.boundary == kFixed, o.periodic_x, o.periodic_y, compute_);
     } else {
       for (int b = 0; b < 2; ++b) {
         t.host[b].assign(n, 0.0f);
@@ -93,6 +148,8 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
         t.scratch[b].assign(n, 0.0f);
       }
       cpu_tile_init(t.g, t.buf[0], o.init);
+      if (o.poison)
+        for (int b = 0; b < 2; ++b) cpu_tile_poison(t.g, t.buf[b], o.boundary == kFixed, o.periodic_x, o.periodic_y);
     }
     tiles_.push_back(std::move(t));
   }
@@ -588,7 +645,9 @@ RunStats Engine::run_impl(int64_t steps) {
       H2D_HIP_CHECK(hipEventRecord(ev_b_[1], compute_));
       if (k > 0) {
         H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_i_[1], 0));
+        trace_begin("exchange", comm_);
         do_exchange_async(k);
+        trace_end("exchange", comm_);
         H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
         ++st.exchanges;
       }
@@ -598,19 +657,25 @@ RunStats Engine::run_impl(int64_t steps) {
         H2D_HIP_CHECK(hipStreamWaitEvent(bstream_, ev_halo_, 0));
         H2D_HIP_CHECK(hipStreamWaitEvent(bstream_, ev_i_[q], 0));
         const int src = tiles_[0].cur;
+        trace_begin("boundary", bstream_);
         for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2, src, bstream_);
+        trace_end("boundary", bstream_);
         H2D_HIP_CHECK(hipEventRecord(ev_b_[p], bstream_));
         for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
         bool check_next = false;
         const int k_next = next_chunk(steps_done_ + k, target, &check_next);
         if (k_next > 0) {
           H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_b_[p], 0));
+          trace_begin("exchange", comm_);
           do_exchange_async(k_next);
+          trace_end("exchange", comm_);
           H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
           ++st.exchanges;
         }
         H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[q], 0));
+        trace_begin("interior", compute_);
         for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1, src, compute_);
+        trace_end("interior", compute_);
         H2D_HIP_CHECK(hipEventRecord(ev_i_[p], compute_));
         ++st.chunks;
         if (check) {
@@ -643,13 +708,17 @@ RunStats Engine::run_impl(int64_t steps) {
       if (k > 0) {
         H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
         H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+        trace_begin("exchange", comm_);
         do_exchange_async(k);
+        trace_end("exchange", comm_);
         H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
         ++st.exchanges;
       }
       while (k > 0) {
         H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+        trace_begin("boundary", compute_);
         for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2);
+        trace_end("boundary", compute_);
         H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
         const int src = tiles_[0].cur;
         for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
@@ -657,11 +726,15 @@ RunStats Engine::run_impl(int64_t steps) {
         const int k_next = next_chunk(steps_done_ + k, target, &check_next);
         if (k_next > 0) {
           H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+          trace_begin("exchange", comm_);
           do_exchange_async(k_next);
+          trace_end("exchange", comm_);
           H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
           ++st.exchanges;
         }
+        trace_begin("interior", compute_);
         for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1, src);
+        trace_end("interior", compute_);
         ++st.chunks;
         if (check) {
           for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
@@ -686,12 +759,16 @@ RunStats Engine::run_impl(int64_t steps) {
         if (has_exchange_) {
           H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
           H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+          trace_begin("exchange", comm_);
           do_exchange_async(k);
+          trace_end("exchange", comm_);
           H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
           H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
           ++st.exchanges;
         }
+        trace_begin("step", compute_);
         advance(k, check);
+        trace_end("step", compute_);
         ++st.chunks;
         if (check) {
           st.residual = finish_residual();
@@ -707,6 +784,7 @@ RunStats Engine::run_impl(int64_t steps) {
     H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
   }
   wait_event(ev_t1_);
+  trace_collect(st);
   float ms = 0.0f;
   H2D_HIP_CHECK(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
   st.device_ms = ms;

@@ -53,6 +53,8 @@ struct EngineOptions {
   int boundary_rows = 16;     // rows per halo-dependent work unit (overlap mode)
   int concurrent = -1;        // boundary units on a second stream: -1 auto, 0 never, 1 always
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
+  bool trace = false;         // per-phase hipEvent timers + roctx ranges
+  bool poison = false;        // debug canary: NaN in every cell no valid update may read
   bool convergence = false;
   int64_t interval = 20;
   double sensitivity = 0.1;
@@ -73,6 +75,8 @@ struct RunStats {
   int64_t chunks = 0;
   int64_t exchanges = 0;
   std::string path;        // "stream", "lds", "naive", "cpu"
+  std::map<std::string, double> phase_ms;    // trace mode: device time per phase (boundary, interior, exchange, step)
+  std::map<std::string, int64_t> phase_count;
 };
 
 class Engine {
@@ -151,6 +155,15 @@ class Engine {
   RunStats run_impl(int64_t steps);
   CopyDesc* local_descs(int K, int& n, int64_t& maxe);
   void check_tile(int t) const;
+  void trace_begin(const char* phase, hipStream_t s);
+  void trace_end(const char* phase, hipStream_t s);
+  void trace_collect(RunStats& st);
+  struct Span {
+    std::string phase;
+    hipEvent_t a, b;
+  };
+  std::vector<Span> spans_;
+  std::map<std::string, hipEvent_t> open_;
 
   EngineOptions opt_;
   Decomposition dec_;

@@ -147,3 +147,20 @@ H2D_HD inline int dim_mode(int64_t g, int64_t N, bool periodic, bool fixed) {
 }
 
 }  // namespace h2d
+
+namespace h2d {
+
+// Debug canary (poison mode): storage cell (i, j) in owned coordinates that no valid update
+// may ever read — padding beyond the ghost ring, and (fixed mode) ghost cells outside the grid.
+// Ghost cells inside the grid are also poisoned: the halo exchange must overwrite them first.
+H2D_HD inline bool poisonable(const TileGeom& g, int64_t i, int64_t j, bool fixed, bool per_x, bool per_y) {
+  if (i >= 0 && i < g.xcell && j >= 0 && j < g.ycell) return false;  // owned
+  const bool in_ring = i >= -g.G && i < g.xcell + g.G && j >= -g.G && j < g.ycell + g.G;
+  if (!in_ring) return true;
+  const int64_t gx = g.gx0 + i, gy = g.gy0 + j;
+  const bool outside = (!per_x && (gx < 0 || gx >= g.NX)) || (!per_y && (gy < 0 || gy >= g.NY));
+  if (outside) return fixed;  // ghost-zero mode reads the zero ring
+  return true;
+}
+
+}  // namespace h2d

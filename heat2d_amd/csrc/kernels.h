@@ -76,6 +76,7 @@ void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hip
 void launch_naive_step(const TileGeom& g, const float* src, float* dst, int precision, int boundary, double cx,
                        double cy, bool per_x, bool per_y, hipStream_t s);
 void launch_init(const TileGeom& g, float* base, int init, hipStream_t s);
+void launch_poison(const TileGeom& g, float* base, bool fixed, bool per_x, bool per_y, hipStream_t s);
 void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s);
 void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s);
 // Residual of a whole tile (Σ (a-b)² over owned cells) — used by tests/ops.

@@ -40,6 +40,14 @@ __global__ void init_kernel(TileGeom g, float* __restrict__ base, int init) {
   }
 }
 
+__global__ void poison_kernel(TileGeom g, float* __restrict__ base, int fixed, int per_x, int per_y) {
+  const int64_t total = g.elems();
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / g.pitch - g.G, j = e % g.pitch - g.PL;
+    if (poisonable(g, i, j, fixed != 0, per_x != 0, per_y != 0)) base[e] = __builtin_nanf("");
+  }
+}
+
 __global__ void copy_rects_kernel(const CopyDesc* __restrict__ descs) {
   const CopyDesc d = descs[blockIdx.y];
   const int64_t total = d.rows * d.cols;
@@ -380,6 +388,13 @@ void launch_init(const TileGeom& g, float* base, int init, hipStream_t s) {
   const int64_t total = g.elems();
   const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 32);
   hipLaunchKernelGGL(init_kernel, dim3(blocks), dim3(256), 0, s, g, base, init);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_poison(const TileGeom& g, float* base, bool fixed, bool per_x, bool per_y, hipStream_t s) {
+  const int64_t total = g.elems();
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 32);
+  hipLaunchKernelGGL(poison_kernel, dim3(blocks), dim3(256), 0, s, g, base, (int)fixed, (int)per_x, (int)per_y);
   H2D_HIP_CHECK(hipGetLastError());
 }
 
