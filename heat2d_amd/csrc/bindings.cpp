@@ -411,6 +411,16 @@ PYBIND11_MODULE(_heat2d, m) {
   m.def("stream_k_supported", &stream_k_supported);
   m.def("lds_solver_fits", &lds_solver_fits);
   m.def("stream_wave_capacity", &stream_wave_capacity);
+  m.def(
+      "unit_plan",
+      [](int64_t nx, int64_t ny, int K, int H, bool fixed, bool per_x, bool per_y, double ew, int64_t capacity) {
+        const TileGeom g = make_tile_geom(nx, ny, 0, 0, nx, ny, K);
+        UnitPlan p = plan_units(g, K, H, fixed, per_x, per_y, ew, capacity, nullptr, 16);
+        py::list out;
+        for (const Unit& u : p.interior) out.append(py::make_tuple(u.strip, u.x0, u.h, u.flags));
+        return out;
+      },
+      "work units (strip, x0, h, flags) of a single nx×ny tile");
   m.def("lead_cols", &lead_cols);
   m.def("strip_out_cols", &strip_out_cols);
 }

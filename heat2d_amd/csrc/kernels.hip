@@ -281,18 +281,20 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<RowRan
   if (H > 0) {
     U = (double)(H + K);
   } else {
-    // Smallest unit cost whose unit count fits one resident round; never below 8 rows.
-    double lo = 8.0 + K, hi = (double)(g.xcell + K) * w + 1.0;
-    if (plan(lo, nullptr) <= capacity) {
-      hi = lo;
-    } else {
-      for (int it = 0; it < 60 && hi - lo > 0.5; ++it) {
-        const double mid = 0.5 * (lo + hi);
-        if (plan(mid, nullptr) <= capacity) hi = mid;
-        else lo = mid;
+    // Minimise the estimated makespan ceil(units / capacity) * U: one full round when the
+    // tile has few strips (the usual case); several full rounds for huge tiles whose strips
+    // alone outnumber the resident waves.  Units never go below 8 rows.
+    const double umin = 8.0 + K, umax = (double)(g.xcell + K) * w + 1.0;
+    double best_u = umax, best_ms = 1e300;
+    for (double u = umin; u <= umax * 1.0001; u *= 1.03) {
+      const int64_t cnt = plan(u, nullptr);
+      const double ms = (double)((cnt + capacity - 1) / std::max<int64_t>(1, capacity)) * u;
+      if (ms < best_ms * 0.999 || (ms <= best_ms * 1.001 && u > best_u)) {
+        best_ms = std::min(best_ms, ms);
+        best_u = u;
       }
     }
-    U = hi;
+    U = best_u;
   }
   std::vector<Unit> v;
   plan(U, &v);

@@ -124,3 +124,25 @@ def test_resume_equals_uninterrupted(native):
     e2.upload(0, mid)
     e2.run(13)
     assert np.array_equal(e2.download(0), native.oracle_run(nx, ny, 30)["grid"])
+
+
+@pytest.mark.parametrize("n,cap", [(37, 1024), (4096, 1024), (4096, 2048), (16384, 1024), (180000, 1024)])
+def test_unit_planner_covers_rows_and_packs_rounds(native, n, cap):
+    K = 8
+    units = native.unit_plan(n, n, K, 0, True, False, False, 1.2, cap)
+    wout = native.strip_out_cols(K)
+    nstrips = (n + wout - 1) // wout
+    rows = {}
+    for s, x0, h, flags in units:
+        rows.setdefault(s, []).append((x0, h))
+    assert sorted(rows) == list(range(nstrips))
+    for s, segs in rows.items():
+        segs.sort()
+        pos = 0
+        for x0, h in segs:
+            assert x0 == pos and h >= 1
+            pos += h
+        assert pos == n
+    # one full round when possible, otherwise nearly-full rounds
+    rounds = -(-len(units) // cap)
+    assert len(units) <= cap or len(units) / (rounds * cap) > 0.9
