@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -45,7 +46,7 @@ def main() -> int:
     ap.add_argument("--boundary", choices=("fixed", "ghost-zero"), default="fixed")
     ap.add_argument("--tblock", type=int, default=8)
     ap.add_argument("--rows-per-wave", type=int, default=0)
-    ap.add_argument("--transport", choices=("auto", "rccl", "torch"), default="auto")
+    ap.add_argument("--transport", choices=("auto", "rccl", "torch", "host"), default="auto")
     ap.add_argument("--layout", choices=("rows", "blocks"), default="rows")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--repeat", type=int, default=1, help="timed repetitions (best reported)")
@@ -90,10 +91,16 @@ def main() -> int:
     run = s.run_steps
     prewarm_steps = 0
     if on_gpu and a.prewarm_s > 0:
-        t_end = time.perf_counter() + a.prewarm_s
-        while time.perf_counter() < t_end:
-            run(64)
-            prewarm_steps += 64
+        # the batch count is agreed collectively: ranks that ran different step counts would
+        # post unmatched halo sends/receives and deadlock
+        sync_barrier()
+        t0 = time.perf_counter()
+        run(64)
+        sync_barrier()
+        t_batch = ctx.allreduce_max(time.perf_counter() - t0)
+        batches = max(0, min(100000, math.ceil(a.prewarm_s / max(t_batch, 1e-6)) - 1))
+        run(64 * batches)
+        prewarm_steps = 64 * (batches + 1)
         sync_barrier()
     if a.warmup > 0:
         run(a.warmup)

@@ -27,44 +27,67 @@ N_DIRS = 8
 
 
 class TorchHaloExchanger:
-    def __init__(self, engine, tile: int = 0, device: Optional[torch.device] = None, group=None):
+    def __init__(self, engine, tile: int = 0, device: Optional[torch.device] = None, group=None,
+                 host_staging: bool = False):
         self.engine = engine
         self.tile = tile
         self.device = device or torch.device("cpu")
         self.group = group
-        self._bufs: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+        # host staging: a GPU engine packs into device buffers, the segments travel through
+        # pinned host copies over the (gloo) group.  Fallback transport, and the way to run
+        # several ranks on one GPU (RCCL refuses duplicate devices in a communicator).
+        self.host_staging = host_staging and self.device.type != "cpu"
+        self._bufs: dict[int, tuple[torch.Tensor, ...]] = {}
         self.opp = list(native().DIR_OPP)
 
     def _buffers(self, k: int):
         if k not in self._bufs:
             ns = max(1, self.engine.send_count(self.tile, k))
             nr = max(1, self.engine.recv_count(self.tile, k))
-            self._bufs[k] = (torch.zeros(ns, dtype=torch.float32, device=self.device),
-                             torch.zeros(nr, dtype=torch.float32, device=self.device))
+            bufs = (torch.zeros(ns, dtype=torch.float32, device=self.device),
+                    torch.zeros(nr, dtype=torch.float32, device=self.device))
+            if self.host_staging:
+                bufs += (torch.zeros(ns, dtype=torch.float32).pin_memory(),
+                         torch.zeros(nr, dtype=torch.float32).pin_memory())
+            self._bufs[k] = bufs
         return self._bufs[k]
 
     def exchange(self, k: int) -> int:
         """Fill the tile's ghost ring to depth k.  Returns the number of messages posted."""
         info = self.engine.plan_info(self.tile, k)
         ent = [info[5 * d:5 * d + 5] for d in range(N_DIRS)]  # peer, send_off, send_n, recv_off, recv_n
-        send, recv = self._buffers(k)
+        bufs = self._buffers(k)
+        dsend, drecv = bufs[0], bufs[1]
+        send, recv = (bufs[2], bufs[3]) if self.host_staging else (dsend, drecv)
         if self.device.type != "cpu":
             torch.cuda.synchronize(self.device)
-        self.engine.pack(self.tile, k, send.data_ptr())
+        self.engine.pack(self.tile, k, dsend.data_ptr())
+        if self.host_staging:
+            torch.cuda.synchronize(self.device)
+            send.copy_(dsend)
+        me = dist.get_rank()
         ops = []
         for d in range(N_DIRS):
             peer, so, sn, _, _ = ent[d]
-            if peer >= 0 and sn > 0:
+            if peer >= 0 and peer != me and sn > 0:
                 ops.append(dist.P2POp(dist.isend, send[so:so + sn], peer, group=self.group, tag=d))
         for d in range(N_DIRS):
             g = self.opp[d]
             peer, _, _, ro, rn = ent[g]
-            if peer >= 0 and rn > 0:
+            if peer == me and rn > 0:
+                # periodic dimension one tile wide: this rank is its own neighbour; the ghost
+                # side g receives this rank's own direction-d segment
+                so, sn = ent[d][1], ent[d][2]
+                assert sn == rn, (d, sn, rn)
+                recv[ro:ro + rn].copy_(send[so:so + sn])
+            elif peer >= 0 and rn > 0:
                 ops.append(dist.P2POp(dist.irecv, recv[ro:ro + rn], peer, group=self.group, tag=d))
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+        if self.host_staging:
+            drecv.copy_(recv)
         if self.device.type != "cpu":
             torch.cuda.synchronize(self.device)
-        self.engine.unpack(self.tile, k, recv.data_ptr())
+        self.engine.unpack(self.tile, k, drecv.data_ptr())
         return len(ops)

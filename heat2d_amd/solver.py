@@ -138,8 +138,9 @@ class Solver:
                 self.engine = self._make_engine(transport, ranks)
         if transport == n.TRANSPORT_EXTERNAL and self.engine.has_exchange():
             dev = torch.device("cuda", self.device) if self.on_gpu else torch.device("cpu")
-            group = self.ctx.get_nccl_group() if self.on_gpu else None
-            self.exchanger = TorchHaloExchanger(self.engine, 0, dev, group)
+            host = cfg.transport == "host"
+            group = self.ctx.get_nccl_group() if self.on_gpu and not host else None
+            self.exchanger = TorchHaloExchanger(self.engine, 0, dev, group, host_staging=self.on_gpu and host)
         if cfg.load:
             full = h2io.read_binary(cfg.load, cfg.nx, cfg.ny)
             for t in range(self.engine.num_tiles()):

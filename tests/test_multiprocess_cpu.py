@@ -67,9 +67,11 @@ def test_gloo_convergence_allreduce(native, tmp_path):
     assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref["grid"])
 
 
-def test_gloo_periodic_blocks(native, tmp_path):
+@pytest.mark.parametrize("n,gx,gy", [(4, 2, 2), (2, 1, 2), (2, 2, 1)])
+def test_gloo_periodic_blocks(native, tmp_path, n, gx, gy):
+    """Periodic dims; a dimension one tile wide makes a rank its own neighbour."""
     nx, ny, steps = 40, 36, 21
-    torchrun(4, ["--nx", str(nx), "--ny", str(ny), "--steps", str(steps), "--gridx", "2", "--gridy", "2",
+    torchrun(n, ["--nx", str(nx), "--ny", str(ny), "--steps", str(steps), "--gridx", str(gx), "--gridy", str(gy),
                  "--periodic", "xy", "--boundary", "ghost-zero", "--output", "binary", "--outdir", str(tmp_path)],
              str(tmp_path))
     ref = native.oracle_run(nx, ny, steps, boundary=1, periodic_x=True, periodic_y=True)["grid"]

@@ -1,0 +1,57 @@
+"""Multi-process runs on one MI355X: several ranks share the card through the ``host``
+transport (gloo point-to-point with pinned host staging; RCCL refuses two ranks on one
+device).  This rehearses the one-process-per-GPU path the bench uses at N > 1 — rank
+device selection, per-rank tiles, timed loop with barrier + max over ranks, collective
+binary output, JSON contract — everything except the RCCL wire itself (covered by the
+RCCL self-exchange tests in ``test_gpu_engine.py``).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests.test_multiprocess_cpu import ROOT, free_port, read_grid
+
+pytestmark = pytest.mark.gpu
+
+
+def _env():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["OMP_NUM_THREADS"] = "1"
+    env["HEAT2D_NO_BUILD"] = "1"
+    return env
+
+
+def _torchrun(n, script_args, cwd, timeout=400):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), *script_args]
+    r = subprocess.run(cmd, cwd=cwd, env=_env(), capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("n,gx,gy,boundary,periodic", [(2, 2, 1, "fixed", "none"), (4, 2, 2, "ghost-zero", "none"),
+                                                       (2, 1, 2, "ghost-zero", "xy")])
+def test_gpu_ranks_host_transport_match_oracle(native, gpu, tmp_path, n, gx, gy, boundary, periodic):
+    nx, ny, steps = 301, 517, 37
+    out = _torchrun(n, ["-m", "heat2d_amd", "--device", "gpu", "--transport", "host", "--nx", str(nx), "--ny", str(ny),
+                        "--steps", str(steps), "--gridx", str(gx), "--gridy", str(gy), "--boundary", boundary,
+                        "--periodic", periodic, "--output", "binary", "--outdir", str(tmp_path)], str(tmp_path))
+    assert f"Starting with {n} processes" in out
+    b = 0 if boundary == "fixed" else 1
+    ref = native.oracle_run(nx, ny, steps, boundary=b, periodic_x="x" in periodic, periodic_y="y" in periodic)["grid"]
+    assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
+
+
+def test_gpu_bench_two_ranks_host_transport(tmp_path):
+    out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "40", "--warmup", "8", "--side",
+                        "1024", "--transport", "host", "--prewarm-s", "0"], str(tmp_path))
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 40 and d["config"]["grid"] == [2048, 1024]
+    assert d["value"] > 0 and d["config"]["transport"] == "host"
