@@ -6,6 +6,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "cpu_reference.h"
 #include "decomposition.h"
 #include "engine.h"
@@ -16,6 +20,40 @@ namespace py = pybind11;
 using namespace h2d;
 
 namespace {
+
+// Work-unit plans of the torch-tensor stencil op, cached per (device, geometry, K, H,
+// precision, boundary): built once with the capacity-aware planner and kept in device
+// memory, so a launch is asynchronous on the caller's stream (no allocation, no sync).
+struct OpPlan {
+  Unit* units = nullptr;
+  int n = 0;
+  float* dummy = nullptr;  // sink for non-output lanes (contents never read)
+};
+
+const OpPlan& op_plan(const TileGeom& g, int K, int H, int precision, bool fixed, bool per_x, bool per_y) {
+  static std::mutex mu;
+  static std::map<std::vector<int64_t>, OpPlan> cache;
+  static std::map<int, float*> dummies;
+  int dev = 0;
+  H2D_HIP_CHECK(hipGetDevice(&dev));
+  const std::vector<int64_t> key{dev,     g.NX,   g.NY, g.xcell, g.ycell,   g.gx0, g.gy0, g.G,  g.PL,
+                                 g.pitch, K,      H,    precision, fixed, per_x, per_y};
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  if (cache.size() > 4096) throw std::runtime_error("op_stream: too many distinct tile geometries");
+  const int64_t cap = stream_wave_capacity(K, precision, dev);
+  std::vector<Unit> u = build_units(g, K, H, fixed, per_x, per_y, 1.2, cap);
+  OpPlan P;
+  P.n = (int)u.size();
+  H2D_HIP_CHECK(hipMalloc(&P.units, std::max<size_t>(1, u.size()) * sizeof(Unit)));
+  H2D_HIP_CHECK(hipMemcpy(P.units, u.data(), u.size() * sizeof(Unit), hipMemcpyHostToDevice));
+  float*& d = dummies[dev];
+  if (!d) H2D_HIP_CHECK(hipMalloc(&d, 4 * kWaveCols * sizeof(float)));
+  P.dummy = d;
+  return cache.emplace(key, P).first->second;
+}
+
 
 py::array_t<float> to_array(const std::vector<float>& v, int64_t rows, int64_t cols) {
   py::array_t<float> a({rows, cols});
@@ -220,7 +258,9 @@ PYBIND11_MODULE(_heat2d, m) {
       .def(py::init([](int64_t nx, int64_t ny, int gridx, int gridy, bool per_x, bool per_y, int boundary,
                        int precision, int init, double cx, double cy, int tblock, int rows_per_wave, bool convergence,
                        int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
-                       bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s, bool trace, bool poison) {
+                       bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s, bool trace, bool poison,
+                       int comm_cus, int contiguous_halo, int comm_cu_layout, int reserve_waves,
+                       bool device_fence_events) {
              EngineOptions o;
              o.nx = nx;
              o.ny = ny;
@@ -251,6 +291,11 @@ PYBIND11_MODULE(_heat2d, m) {
              o.watchdog_s = watchdog_s;
              o.trace = trace;
              o.poison = poison;
+             o.comm_cus = comm_cus;
+             o.contiguous_halo = contiguous_halo;
+             o.comm_cu_layout = comm_cu_layout;
+             o.reserve_waves = reserve_waves;
+             o.device_fence_events = device_fence_events;
              return new Engine(o);
            }),
            py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
@@ -260,14 +305,19 @@ PYBIND11_MODULE(_heat2d, m) {
            py::arg("interval") = 20, py::arg("sensitivity") = 0.1, py::arg("device") = 0,
            py::arg("ranks") = std::vector<int>{}, py::arg("transport") = (int)kTransportAuto,
            py::arg("overlap") = true, py::arg("small_grid_lds") = true, py::arg("naive") = false,
-           py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0, py::arg("concurrent") = -1, py::arg("boundary_rows") = 16,
-           py::arg("watchdog_s") = 900.0, py::arg("trace") = false, py::arg("poison") = false)
+           py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0, py::arg("concurrent") = -1, py::arg("boundary_rows") = 8,
+           py::arg("watchdog_s") = 900.0, py::arg("trace") = false, py::arg("poison") = false,
+           py::arg("comm_cus") = -1, py::arg("contiguous_halo") = -1, py::arg("comm_cu_layout") = 0, py::arg("reserve_waves") = -1,
+           py::arg("device_fence_events") = false)
       .def("num_tiles", &Engine::num_tiles)
       .def("tile_rank", &Engine::tile_rank)
       .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })
       .def("halo_depth", &Engine::halo_depth)
       .def("has_exchange", &Engine::has_exchange)
       .def("concurrent", &Engine::concurrent)
+      .def("comm_cus", &Engine::comm_cus)
+      .def("contiguous_halo", &Engine::contiguous_halo)
+      .def("wave_capacity", &Engine::wave_capacity)
       .def("on_gpu", &Engine::on_gpu)
       .def("rows_per_wave", &Engine::rows_per_wave)
       .def("num_units", &Engine::num_units)
@@ -357,17 +407,12 @@ PYBIND11_MODULE(_heat2d, m) {
         const TileGeom g = geom_from(geom);
         if (!stream_k_supported(K)) throw std::invalid_argument("unsupported K");
         if (K > g.G) throw std::invalid_argument("K exceeds the tile's ghost depth");
-        if (H <= 0) H = 64;
-        std::vector<Unit> u = build_units(g, K, H, boundary == kFixed, per_x, per_y, 1.0, 1 << 30);
-        Unit* du = nullptr;
-        hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-        H2D_HIP_CHECK(hipMalloc(&du, u.size() * sizeof(Unit)));
-        H2D_HIP_CHECK(hipMemcpy(du, u.data(), u.size() * sizeof(Unit), hipMemcpyHostToDevice));
+        const OpPlan& P = op_plan(g, K, H, precision, boundary == kFixed, per_x, per_y);
         StreamArgs a;
         a.src = reinterpret_cast<const float*>(src);
         a.dst = reinterpret_cast<float*>(dst);
-        a.units = du;
-        a.nunits = (int)u.size();
+        a.units = P.units;
+        a.nunits = P.n;
         a.R = (int)lead_cols(K);
         a.wout = (int)strip_out_cols(K);
         a.pitch = g.pitch;
@@ -385,19 +430,23 @@ PYBIND11_MODULE(_heat2d, m) {
         a.per_x = per_x;
         a.per_y = per_y;
         a.partials = reinterpret_cast<double*>(partials);
-        float* dummy = nullptr;
-        H2D_HIP_CHECK(hipMalloc(&dummy, 4 * kWaveCols * sizeof(float)));
-        a.dummy = dummy;
-        launch_stream(a, K, precision, partials != 0, s);
-        H2D_HIP_CHECK(hipStreamSynchronize(s));
-        H2D_HIP_CHECK(hipFree(du));
-        H2D_HIP_CHECK(hipFree(dummy));
-        return (int)u.size();
+        a.dummy = P.dummy;
+        launch_stream(a, K, precision, partials != 0, reinterpret_cast<hipStream_t>(stream));
+        return P.n;
       },
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("K"), py::arg("precision") = (int)kRef,
       py::arg("boundary") = (int)kFixed, py::arg("cx") = kCxDouble, py::arg("cy") = kCxDouble,
-      py::arg("periodic_x") = false, py::arg("periodic_y") = false, py::arg("H") = 64, py::arg("partials") = 0,
+      py::arg("periodic_x") = false, py::arg("periodic_y") = false, py::arg("H") = 0, py::arg("partials") = 0,
       py::arg("stream") = 0);
+  m.def(
+      "op_num_units",
+      [](const py::dict& geom, int K, int precision, int boundary, bool per_x, bool per_y, int H) {
+        const TileGeom g = geom_from(geom);
+        if (!stream_k_supported(K)) throw std::invalid_argument("unsupported K");
+        return op_plan(g, K, H, precision, boundary == kFixed, per_x, per_y).n;
+      },
+      py::arg("geom"), py::arg("K"), py::arg("precision") = (int)kRef, py::arg("boundary") = (int)kFixed,
+      py::arg("periodic_x") = false, py::arg("periodic_y") = false, py::arg("H") = 0);
   m.def(
       "op_naive",
       [](uintptr_t src, uintptr_t dst, const py::dict& geom, int precision, int boundary, double cx, double cy,

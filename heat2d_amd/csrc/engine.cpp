@@ -113,12 +113,36 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
   if (transport_ == kTransportRccl && ranks.size() != 1) throw std::invalid_argument("RCCL transport: one tile per process");
   if (transport_ == kTransportRccl && !on_gpu()) throw std::invalid_argument("RCCL transport needs a GPU");
 
+  contig_ = transport_ == kTransportRccl && o.contiguous_halo != 0 && o.gridy == 1 && !o.periodic_y;
   if (on_gpu()) {
     H2D_HIP_CHECK(hipSetDevice(o.device));
-    H2D_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
-    H2D_HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
-    H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
-    H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+    hipDeviceProp_t prop;
+    H2D_HIP_CHECK(hipGetDeviceProperties(&prop, o.device));
+    device_cus_ = std::max(1, prop.multiProcessorCount);
+    // auto: off (measured: masked compute queues ran the stencil ~2x slower on gfx950)
+    comm_cus_ = o.comm_cus < 0 ? 0 : o.comm_cus;
+    if (comm_cus_ >= device_cus_ / 2) comm_cus_ = 0;
+    if (comm_cus_ > 0) {
+      std::vector<uint32_t> mc((device_cus_ + 31) / 32, 0u), mx(mc.size(), 0u);
+      std::vector<char> res(device_cus_, 0);
+      for (int i = 0; i < comm_cus_; ++i) {
+        const int c = o.comm_cu_layout == 1 ? device_cus_ - 1 - i
+                      : o.comm_cu_layout == 2 ? i
+                                              : (int)((int64_t)(i + 1) * device_cus_ / comm_cus_ - 1);
+        res[c] = 1;
+      }
+      for (int c = 0; c < device_cus_; ++c) (res[c] ? mx : mc)[c / 32] |= 1u << (c % 32);
+      H2D_HIP_CHECK(hipExtStreamCreateWithCUMask(&compute_, (uint32_t)mc.size(), mc.data()));
+      H2D_HIP_CHECK(hipExtStreamCreateWithCUMask(&comm_, (uint32_t)mx.size(), mx.data()));
+    } else {
+      H2D_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+      H2D_HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+    }
+    // Pipeline events only order work on this device (RCCL fences its own cross-device
+    // traffic), so they can skip the system-scope fence.
+    const unsigned evf = hipEventDisableTiming | (o.device_fence_events ? hipEventDisableSystemFence : 0u);
+    H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, evf));
+    H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, evf));
     H2D_HIP_CHECK(hipEventCreate(&ev_t0_));
     H2D_HIP_CHECK(hipEventCreate(&ev_t1_));
     d_resid_ = dmalloc<double>(ranks.size() + 1);
@@ -169,8 +193,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       } else {
         int64_t nb = 0;
         for (int t = 0; t < (int)tiles_.size(); ++t) nb += units(t, G_).n_boundary;
-        const int64_t cap = opt_.wave_capacity > 0 ? opt_.wave_capacity : stream_wave_capacity(G_, opt_.precision, opt_.device);
-        concurrent_ = nb * 8 <= cap;
+        concurrent_ = nb * 8 <= wave_capacity(G_);
         for (auto& kv : units_) {
           hipFree(kv.second.d_all);
           hipFree(kv.second.d_interior);
@@ -180,10 +203,17 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       }
     }
     if (concurrent_) {
-      H2D_HIP_CHECK(hipStreamCreateWithFlags(&bstream_, hipStreamNonBlocking));
+      if (comm_cus_ > 0) {
+        std::vector<uint32_t> m(4096 / 32);
+        H2D_HIP_CHECK(hipExtStreamGetCUMask(compute_, (uint32_t)m.size(), m.data()));
+        H2D_HIP_CHECK(hipExtStreamCreateWithCUMask(&bstream_, (uint32_t)m.size(), m.data()));
+      } else {
+        H2D_HIP_CHECK(hipStreamCreateWithFlags(&bstream_, hipStreamNonBlocking));
+      }
       for (int i = 0; i < 2; ++i) {
-        H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_i_[i], hipEventDisableTiming));
-        H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_b_[i], hipEventDisableTiming));
+        const unsigned evf = hipEventDisableTiming | (o.device_fence_events ? hipEventDisableSystemFence : 0u);
+        H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_i_[i], evf));
+        H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_b_[i], evf));
       }
     }
     for (int t = 0; t < (int)tiles_.size(); ++t)
@@ -233,6 +263,12 @@ void Engine::check_tile(int t) const {
   if (t < 0 || t >= (int)tiles_.size()) throw std::out_of_range("tile index");
 }
 
+int64_t Engine::wave_capacity(int K) const {
+  if (opt_.wave_capacity > 0) return opt_.wave_capacity;
+  const int64_t cap = stream_wave_capacity(K, opt_.precision, opt_.device);
+  return comm_cus_ > 0 ? cap * (device_cus_ - comm_cus_) / device_cus_ : cap;
+}
+
 int Engine::rows_per_wave(int K) const {
   auto it = units_.find(std::make_pair(0, K));
   if (it != units_.end()) return it->second.H;
@@ -257,12 +293,17 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   UnitLists L;
   bool peer[kNumDirs];
   for (int d = 0; d < kNumDirs; ++d) peer[d] = dec_.neighbor(tl.rank, d) >= 0;
-  const int64_t cap = opt_.wave_capacity > 0 ? opt_.wave_capacity : stream_wave_capacity(K, opt_.precision, opt_.device);
+  const int64_t cap = wave_capacity(K);
   UnitPlan P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                           opt_.edge_weight, cap, peer, opt_.boundary_rows);
-  if (concurrent_ && !P.boundary.empty()) {
-    // boundary and interior launches are co-resident: interior units fill what is left
-    const int64_t cap_in = std::max<int64_t>(cap / 2, cap - (int64_t)P.boundary.size());
+  // auto headroom (4096^2 row-periodic RCCL self-exchange, us/step: 14.3 -> 10.4-10.9 with
+  // 16 in the concurrent pipeline; 14.3 -> 12.6 with 32 in the boundary-first one)
+  const int64_t reserve = opt_.reserve_waves >= 0 ? opt_.reserve_waves : (concurrent_ ? 16 : 32);
+  if (has_exchange_ && opt_.overlap && !P.boundary.empty() && (concurrent_ || reserve > 0)) {
+    // interior units leave room for what runs beside them: the boundary units (concurrent
+    // pipeline) and the exchange kernels
+    const int64_t nb = concurrent_ ? (int64_t)P.boundary.size() : 0;
+    const int64_t cap_in = std::max<int64_t>(cap / 2, cap - nb - reserve);
     P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                    opt_.edge_weight, cap_in, peer, opt_.boundary_rows);
   }
@@ -426,6 +467,31 @@ void Engine::do_exchange_async(int K) {
   if (transport_ != kTransportRccl) throw std::logic_error("do_exchange_async: transport");
   if (!rccl_comm_) throw std::runtime_error("RCCL transport selected but init_rccl() was not called");
   Tile& T = tiles_[0];
+  ncclComm_t comm = (ncclComm_t)rccl_comm_;
+  if (contig_) {
+    // 1-D row strips: every tile has the full row width and the same pitch, so a K-deep
+    // halo is K consecutive storage rows (the west/east pad columns lie outside the global
+    // grid and are never read by a valid update).  Send owned rows [0,K) north and
+    // [xcell-K,xcell) south; receive straight into ghost rows [-K,0) and [xcell,xcell+K).
+    // Same posting order as the general path (sends N,S; receives for ghost S,N).
+    const TileGeom& g = T.g;
+    float* b = T.buf[T.cur];
+    const size_t cnt = (size_t)K * (size_t)g.pitch;
+    const int pn = dec_.neighbor(T.rank, kN), ps = dec_.neighbor(T.rank, kS);
+    auto row = [&](int64_t i) { return b + (size_t)(i + g.G) * (size_t)g.pitch; };
+    H2D_NCCL_CHECK(ncclGroupStart());
+    for (int d = 0; d < kNumDirs; ++d) {
+      if (d == kN && pn >= 0) H2D_NCCL_CHECK(ncclSend(row(0), cnt, ncclFloat, pn, comm, comm_));
+      if (d == kS && ps >= 0) H2D_NCCL_CHECK(ncclSend(row(g.xcell - K), cnt, ncclFloat, ps, comm, comm_));
+    }
+    for (int d = 0; d < kNumDirs; ++d) {
+      const int gs = kDirOpp[d];
+      if (gs == kN && pn >= 0) H2D_NCCL_CHECK(ncclRecv(row(-K), cnt, ncclFloat, pn, comm, comm_));
+      if (gs == kS && ps >= 0) H2D_NCCL_CHECK(ncclRecv(row(g.xcell), cnt, ncclFloat, ps, comm, comm_));
+    }
+    H2D_NCCL_CHECK(ncclGroupEnd());
+    return;
+  }
   ExchangePlan p = make_plan(dec_, T.rank, T.g, K);
   if (p.send_total > stage_cap_ || p.recv_total > stage_cap_) {
     H2D_HIP_CHECK(hipStreamSynchronize(comm_));
@@ -456,7 +522,6 @@ void Engine::do_exchange_async(int K) {
   }
   auto iu = unpack_descs_.find(key);
   launch_copy_rects(std::get<0>(ip->second), std::get<1>(ip->second), std::get<2>(ip->second), comm_);
-  ncclComm_t comm = (ncclComm_t)rccl_comm_;
   H2D_NCCL_CHECK(ncclGroupStart());
   // Send segment d to peer[d]; receive the peer's matching segment into ghost side opp(d)
   // from peer[opp(d)].  Posting both in direction order keeps per-peer FIFO matching

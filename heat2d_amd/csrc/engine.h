@@ -50,7 +50,7 @@ struct EngineOptions {
   int rows_per_wave = 0;   // H; 0 = automatic
   double edge_weight = 1.2;  // relative cost of a global-edge work unit (load balance)
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
-  int boundary_rows = 16;     // rows per halo-dependent work unit (overlap mode)
+  int boundary_rows = 8;      // rows per halo-dependent work unit (overlap mode; at least K)
   int concurrent = -1;        // boundary units on a second stream: -1 auto, 0 never, 1 always
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
@@ -64,6 +64,20 @@ struct EngineOptions {
   bool overlap = true;     // overlap halo exchange with interior compute
   bool small_grid_lds = true;  // whole-grid LDS solver for small single-tile problems
   bool naive = false;      // validation: one-thread-per-cell single-step kernel
+  // CUs reserved for the comm stream (pack/unpack/RCCL kernels) when halos are exchanged;
+  // the compute streams are masked to the other CUs so the exchange kernels never wait for
+  // resident stencil waves to drain.  -1 auto, 0 off.
+  int comm_cus = -1;
+  int comm_cu_layout = 0;
+  // Resident-wave slots the interior launch leaves free for kernels that run beside it (the
+  // RCCL p2p kernel and, in the concurrent pipeline, the boundary units).  The dispatcher
+  // deals waves round-robin over XCDs and shader engines, so a kernel launched second only
+  // finds a slot if every engine keeps some free.  -1 auto.
+  int reserve_waves = -1;
+  bool device_fence_events = false;  // pipeline events without the system-scope fence  // reserved CU indices: 0 spread evenly, 1 the highest, 2 the lowest
+  // RCCL: send/receive whole K-row halos straight from/into the tile (no pack/unpack) when
+  // the decomposition has no west/east neighbours (1-D row strips).  -1 auto, 0 off.
+  int contiguous_halo = -1;
 };
 
 struct RunStats {
@@ -99,6 +113,9 @@ class Engine {
   int num_units(int K) const;      // work units (waves) per chunk of depth K, all tiles
   int64_t steps_done() const { return steps_done_; }
   uintptr_t stream_handle() const { return (uintptr_t)compute_; }
+  int comm_cus() const { return comm_cus_; }
+  bool contiguous_halo() const { return contig_; }
+  int64_t wave_capacity(int K) const;  // resident waves available to the compute streams
 
   // RCCL bootstrap: rank 0 creates the id, the caller broadcasts it (torch.distributed).
   static std::string rccl_unique_id();
@@ -189,6 +206,8 @@ class Engine {
   float* d_send_ = nullptr;
   float* d_recv_ = nullptr;
   int64_t stage_cap_ = 0;
+  int comm_cus_ = 0, device_cus_ = 0;
+  bool contig_ = false;
   void* rccl_comm_ = nullptr;       // ncclComm_t
   int rccl_rank_ = 0, rccl_nranks_ = 1;
 };

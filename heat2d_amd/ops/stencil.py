@@ -58,12 +58,14 @@ def init_tile(t: torch.Tensor, g: dict, init: str = "exact") -> torch.Tensor:
 
 def stencil(src: torch.Tensor, dst: torch.Tensor, g: dict, K: int = 1, *, precision: str = "ref",
             boundary: str = "fixed", cx: float = 0.1, cy: float = 0.1, periodic: Tuple[bool, bool] = (False, False),
-            rows_per_wave: int = 64, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+            rows_per_wave: int = 0, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K fused time steps src -> dst with the streaming kernel (owned cells of dst written).
 
+    Asynchronous on the current torch stream: the work-unit plan (``rows_per_wave`` 0 = sized
+    to the resident-wave capacity) is built once per geometry and cached on the device.
     Periodic dimensions need their ghost ring filled by the caller (``fill_periodic_ghosts``).
-    ``residual``: optional float64 tensor of at least `num_units` elements receiving per-wave
-    partial sums of (u_K - u_{K-1})^2."""
+    ``residual``: optional float64 tensor of at least ``num_units(...)`` elements receiving
+    per-wave partial sums of (u_K - u_{K-1})^2."""
     _check(src, g)
     _check(dst, g)
     if K > g["G"]:
@@ -72,10 +74,20 @@ def stencil(src: torch.Tensor, dst: torch.Tensor, g: dict, K: int = 1, *, precis
     if residual is not None:
         if residual.dtype != torch.float64 or residual.device != src.device:
             raise ValueError("residual must be a float64 tensor on the same device")
+        need = num_units(g, K, precision=precision, boundary=boundary, periodic=periodic, rows_per_wave=rows_per_wave)
+        if residual.numel() < need or not residual.is_contiguous():
+            raise ValueError(f"residual needs at least {need} contiguous elements")
         part = residual.data_ptr()
     native().op_stream(src.data_ptr(), dst.data_ptr(), g, K, PRECISIONS[precision], BOUNDARIES[boundary], cx, cy,
                        periodic[0], periodic[1], rows_per_wave, part, _stream())
     return dst
+
+
+def num_units(g: dict, K: int, *, precision: str = "ref", boundary: str = "fixed",
+              periodic: Tuple[bool, bool] = (False, False), rows_per_wave: int = 0) -> int:
+    """Waves (work units) of one ``stencil`` launch = residual partials it writes."""
+    return native().op_num_units(g, K, PRECISIONS[precision], BOUNDARIES[boundary], periodic[0], periodic[1],
+                                 rows_per_wave)
 
 
 def naive_step(src: torch.Tensor, dst: torch.Tensor, g: dict, *, precision: str = "ref", boundary: str = "fixed",

@@ -189,10 +189,16 @@ def test_concurrent_auto_for_row_strips(native, gpu):
 
 
 @pytest.mark.parametrize("concurrent", [0, 1])
-def test_rccl_self_exchange_row_periodic(native, gpu, concurrent):
-    nx, ny, steps = 300, 700, 37
-    eng = native.Engine(nx, ny, periodic_x=True, boundary=1, device=gpu, ranks=[0], transport=native.TRANSPORT_RCCL,
-                        concurrent=concurrent)
+@pytest.mark.parametrize("contig,comm_cus", [(0, 0), (1, 0), (1, 8), (0, 4)])
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_rccl_self_exchange_row_periodic(native, gpu, concurrent, contig, comm_cus, boundary):
+    """Row-periodic single rank: the per-rank shape of the 1-D row-strip bench.  Covers the
+    contiguous K-row halo path (no pack/unpack) and CU-partitioned comm/compute streams."""
+    nx, ny, steps = 300, 701, 37
+    eng = native.Engine(nx, ny, periodic_x=True, boundary=boundary, device=gpu, ranks=[0],
+                        transport=native.TRANSPORT_RCCL, concurrent=concurrent, contiguous_halo=contig,
+                        comm_cus=comm_cus, poison=True)
+    assert eng.contiguous_halo() == bool(contig) and eng.comm_cus() == comm_cus
     eng.init_rccl(native.Engine.rccl_unique_id(), 1, 0)
     eng.run(steps)
-    assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, 1, per=(True, False))["grid"])
+    assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, boundary, per=(True, False))["grid"])
