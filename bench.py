@@ -144,8 +144,7 @@ def main() -> int:
                 "global_batch": nx * ny,
                 "seq_len": a.steps,
                 "parallelism": (f"rows{gx}" if a.layout == "rows" else f"blocks{gx}x{gy}") if world > 1 else "single",
-                "overlap": ("none" if not s.engine.has_exchange() else
-                            "concurrent" if s.engine.concurrent() else ("boundary-first" if cfg.overlap else "off")),
+                "overlap": s.engine.pipeline(),
                 "tblock": s.engine.halo_depth(),
                 "path": res["path"],
                 "transport": cfg.transport,

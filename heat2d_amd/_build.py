@@ -3,7 +3,7 @@
 Every translation unit is compiled by ``hipcc --offload-arch=gfx950`` with
 ``-ffp-contract=off`` (the bit-exact numerics contract).  The streaming
 stencil is instantiated once per temporal-block depth K in its own translation unit so the
-objects compile in parallel.  Objects are rebuilt only when a source or header is newer.
+objects compile in parallel.  Objects are rebuilt only when the source or a header it includes is newer.
 
 Usage: ``python -m heat2d_amd._build [--force] [--jobs N]``.
 """
@@ -12,6 +12,7 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -63,11 +64,20 @@ def _py_includes() -> list[str]:
     return [f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}"]
 
 
-def _headers_mtime() -> float:
-    m = 0.0
-    for f in os.listdir(CSRC):
-        if f.endswith((".h", ".hpp")):
-            m = max(m, os.path.getmtime(os.path.join(CSRC, f)))
+_INCLUDE_RE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _deps_mtime(src: str, seen: set | None = None) -> float:
+    """Newest mtime over `src` and the in-tree headers it includes, transitively."""
+    seen = set() if seen is None else seen
+    path = os.path.join(CSRC, src)
+    if src in seen or not os.path.exists(path):
+        return 0.0
+    seen.add(src)
+    m = os.path.getmtime(path)
+    with open(path, encoding="utf-8", errors="replace") as f:
+        for inc in _INCLUDE_RE.findall(f.read()):
+            m = max(m, _deps_mtime(inc, seen))
     return m
 
 
@@ -75,11 +85,11 @@ def _obj_for(src: str) -> str:
     return os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
 
 
-def _compile(src: str, force: bool, hmtime: float) -> tuple[str, bool]:
+def _compile(src: str, force: bool) -> tuple[str, bool]:
     path = os.path.join(CSRC, src)
     obj = _obj_for(src)
     if not force and os.path.exists(obj):
-        if os.path.getmtime(obj) >= max(os.path.getmtime(path), hmtime):
+        if os.path.getmtime(obj) >= _deps_mtime(src):
             return obj, False
     cmd = [_hipcc(), *COMMON_FLAGS, f"-I{CSRC}"]
     if src == "bindings.cpp":
@@ -107,13 +117,12 @@ def build(force: bool = False, jobs: int | None = None, cli: bool = True, verbos
     """Compile (incrementally) and link the extension and the CLI.  Returns the extension path."""
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(os.path.dirname(CLI_PATH), exist_ok=True)
-    hm = _headers_mtime()
     srcs = sorted(set(EXT_SOURCES + (CLI_SOURCES if cli else [])))
     srcs = [s for s in srcs if os.path.exists(os.path.join(CSRC, s))]
     jobs = jobs or max(1, min(8, os.cpu_count() or 1))
     rebuilt = []
     with cf.ThreadPoolExecutor(jobs) as ex:
-        futs = {ex.submit(_compile, s, force, hm): s for s in srcs}
+        futs = {ex.submit(_compile, s, force): s for s in srcs}
         for f in cf.as_completed(futs):
             obj, did = f.result()
             if did:

@@ -260,7 +260,7 @@ PYBIND11_MODULE(_heat2d, m) {
                        int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
                        bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s, bool trace, bool poison,
                        int comm_cus, int contiguous_halo, int comm_cu_layout, int reserve_waves,
-                       bool device_fence_events) {
+                       bool device_fence_events, int comm_boundary, int signal_exchange, int device_halo_wait) {
              EngineOptions o;
              o.nx = nx;
              o.ny = ny;
@@ -296,6 +296,9 @@ PYBIND11_MODULE(_heat2d, m) {
              o.comm_cu_layout = comm_cu_layout;
              o.reserve_waves = reserve_waves;
              o.device_fence_events = device_fence_events;
+             o.comm_boundary = comm_boundary;
+             o.signal_exchange = signal_exchange;
+             o.device_halo_wait = device_halo_wait;
              return new Engine(o);
            }),
            py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
@@ -308,13 +311,15 @@ PYBIND11_MODULE(_heat2d, m) {
            py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0, py::arg("concurrent") = -1, py::arg("boundary_rows") = 8,
            py::arg("watchdog_s") = 900.0, py::arg("trace") = false, py::arg("poison") = false,
            py::arg("comm_cus") = -1, py::arg("contiguous_halo") = -1, py::arg("comm_cu_layout") = 0, py::arg("reserve_waves") = -1,
-           py::arg("device_fence_events") = false)
+           py::arg("device_fence_events") = false, py::arg("comm_boundary") = -1, py::arg("signal_exchange") = -1, py::arg("device_halo_wait") = -1)
       .def("num_tiles", &Engine::num_tiles)
       .def("tile_rank", &Engine::tile_rank)
       .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })
       .def("halo_depth", &Engine::halo_depth)
       .def("has_exchange", &Engine::has_exchange)
       .def("concurrent", &Engine::concurrent)
+      .def("signal_mode", &Engine::signal_mode)
+      .def("pipeline", &Engine::pipeline)
       .def("comm_cus", &Engine::comm_cus)
       .def("contiguous_halo", &Engine::contiguous_halo)
       .def("wave_capacity", &Engine::wave_capacity)

@@ -184,10 +184,39 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       tiles_[t].pcap = 256;
       tiles_[t].partials = dmalloc<double>(256);
     }
+    // Signalled pipeline (default with an exchange): one launch per chunk, halo-dependent
+    // units first, the exchange gated mid-kernel on their completion counter.
+    sig_mode_ = 0;
+    if (has_exchange_ && opt_.overlap && !opt_.naive && opt_.signal_exchange != 0) {
+      sig_mode_ = opt_.signal_exchange < 0 ? 2 : opt_.signal_exchange;
+      if (sig_mode_ == 1) {
+        int ok = 0;
+        hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, o.device);
+        if (!ok) sig_mode_ = 2;
+      }
+      if (sig_mode_ == 1 &&
+          hipExtMallocWithFlags(reinterpret_cast<void**>(&sig_counter_), sizeof(unsigned long long),
+                                hipMallocSignalMemory) != hipSuccess) {
+        (void)hipGetLastError();
+        sig_counter_ = nullptr;
+        sig_mode_ = 2;  // no signal memory: polling-kernel gate
+      }
+      if (sig_mode_ == 2) {
+        sig_counter_ = dmalloc<unsigned long long>(8);
+      }
+      H2D_HIP_CHECK(hipMemset(sig_counter_, 0, sizeof(unsigned long long)));
+      d_sig_timeout_ = dmalloc<unsigned int>(1);
+      H2D_HIP_CHECK(hipMemset(d_sig_timeout_, 0, sizeof(unsigned int)));
+      dev_wait_ = opt_.device_halo_wait != 0;
+      if (dev_wait_) {
+        halo_counter_ = dmalloc<unsigned long long>(8);
+        H2D_HIP_CHECK(hipMemset(halo_counter_, 0, sizeof(unsigned long long)));
+      }
+    }
     // Overlap mode: run the halo-dependent boundary units CONCURRENTLY with the interior
     // (second stream) when they are few — e.g. 1-D row decompositions — otherwise first.
     concurrent_ = false;
-    if (has_exchange_ && opt_.overlap && opt_.concurrent != 0) {
+    if (has_exchange_ && opt_.overlap && opt_.concurrent != 0 && sig_mode_ == 0) {
       if (opt_.concurrent > 0) {
         concurrent_ = true;
       } else {
@@ -198,6 +227,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
           hipFree(kv.second.d_all);
           hipFree(kv.second.d_interior);
           hipFree(kv.second.d_boundary);
+          hipFree(kv.second.d_bfirst);
         }
         units_.clear();
       }
@@ -236,7 +266,11 @@ Engine::~Engine() {
     hipFree(kv.second.d_all);
     hipFree(kv.second.d_interior);
     hipFree(kv.second.d_boundary);
+    hipFree(kv.second.d_bfirst);
   }
+  hipFree(sig_counter_);
+  hipFree(d_sig_timeout_);
+  hipFree(halo_counter_);
   for (auto* m : {&local_descs_, &pack_descs_, &unpack_descs_})
     for (auto& kv : *m) hipFree(std::get<0>(kv.second));
   for (auto& t : tiles_) hipFree(t.partials);
@@ -298,11 +332,11 @@ const Engine::UnitLists& Engine::units(int t, int K) {
                           opt_.edge_weight, cap, peer, opt_.boundary_rows);
   // auto headroom (4096^2 row-periodic RCCL self-exchange, us/step: 14.3 -> 10.4-10.9 with
   // 16 in the concurrent pipeline; 14.3 -> 12.6 with 32 in the boundary-first one)
-  const int64_t reserve = opt_.reserve_waves >= 0 ? opt_.reserve_waves : (concurrent_ ? 16 : 32);
-  if (has_exchange_ && opt_.overlap && !P.boundary.empty() && (concurrent_ || reserve > 0)) {
+  const int64_t reserve = opt_.reserve_waves >= 0 ? opt_.reserve_waves : ((concurrent_ || sig_mode_ > 0) ? 16 : 32);
+  if (has_exchange_ && opt_.overlap && !P.boundary.empty() && (concurrent_ || sig_mode_ > 0 || reserve > 0)) {
     // interior units leave room for what runs beside them: the boundary units (concurrent
-    // pipeline) and the exchange kernels
-    const int64_t nb = concurrent_ ? (int64_t)P.boundary.size() : 0;
+    // and signalled pipelines) and the exchange kernels
+    const int64_t nb = (concurrent_ || sig_mode_ > 0) ? (int64_t)P.boundary.size() : 0;
     const int64_t cap_in = std::max<int64_t>(cap / 2, cap - nb - reserve);
     P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                    opt_.edge_weight, cap_in, peer, opt_.boundary_rows);
@@ -324,6 +358,10 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     H2D_HIP_CHECK(hipMemcpy(L.d_all, all.data(), all.size() * sizeof(Unit), hipMemcpyHostToDevice));
     if (!in.empty()) H2D_HIP_CHECK(hipMemcpy(L.d_interior, in.data(), in.size() * sizeof(Unit), hipMemcpyHostToDevice));
     if (!bd.empty()) H2D_HIP_CHECK(hipMemcpy(L.d_boundary, bd.data(), bd.size() * sizeof(Unit), hipMemcpyHostToDevice));
+    std::vector<Unit> bfirst = bd;
+    bfirst.insert(bfirst.end(), in.begin(), in.end());
+    L.d_bfirst = dmalloc<Unit>(bfirst.size());
+    H2D_HIP_CHECK(hipMemcpy(L.d_bfirst, bfirst.data(), bfirst.size() * sizeof(Unit), hipMemcpyHostToDevice));
     Tile& tw = tiles_[t];
     if ((int64_t)all.size() > tw.pcap) {
       H2D_HIP_CHECK(hipDeviceSynchronize());
@@ -367,13 +405,26 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   } else if (which == 1) {
     a.units = L.d_interior;
     a.nunits = L.n_interior;
-  } else {
+  } else if (which == 2) {
     a.units = L.d_boundary;
     a.nunits = L.n_boundary;
     a.partials = tl.partials + L.n_interior;
+  } else {
+    a.units = L.d_bfirst;
+    a.nunits = L.n_all;
+    a.prot = L.n_interior;
+    a.signal = sig_counter_;
+    a.nsignal = L.n_boundary;
+    sig_target_ += (unsigned long long)L.n_boundary;
+    if (dev_wait_) {
+      a.halo_ready = halo_counter_;
+      a.halo_need = halo_seq_;
+      a.halo_polls = 20000000LL;  // ~1-2 us per system-scope poll: gives up after tens of seconds
+      a.timed_out = d_sig_timeout_;
+    }
   }
   launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
-  if (residual && which == 0) reduce_tile_residual(t, K);
+  if (residual && (which == 0 || which == 3)) reduce_tile_residual(t, K);
 }
 
 void Engine::reduce_tile_residual(int t, int K) {
@@ -539,6 +590,32 @@ void Engine::do_exchange_async(int K) {
   launch_copy_rects(std::get<0>(iu->second), std::get<1>(iu->second), std::get<2>(iu->second), comm_);
 }
 
+void Engine::gate_exchange() {
+  // comm stream: everything after this waits until every halo-dependent unit launched so far
+  // has released its rows
+  if (sig_mode_ == 1) {
+    H2D_HIP_CHECK(hipStreamWaitValue64(comm_, sig_counter_, sig_target_, hipStreamWaitValueGte));
+  } else {
+    // ~0.5 us per poll: gives up after ~30 s (reported at the end of the run)
+    launch_wait_counter(sig_counter_, sig_target_, d_sig_timeout_, 60000000LL, comm_);
+  }
+}
+
+void Engine::exchange_landed() {
+  if (dev_wait_) {
+    launch_set_counter(halo_counter_, ++halo_seq_, comm_);
+  } else {
+    H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
+  }
+}
+
+std::string Engine::pipeline() const {
+  if (!has_exchange_) return "none";
+  if (sig_mode_ > 0) return "signal";
+  if (concurrent_) return opt_.comm_boundary != 0 ? "concurrent" : "concurrent3";
+  return opt_.overlap ? "boundary-first" : "serial";
+}
+
 void Engine::advance(int k, bool residual) {
   if (k < 1 || k > G_) throw std::invalid_argument("advance: chunk size must be in [1, halo depth]");
   for (int t = 0; t < (int)tiles_.size(); ++t) {
@@ -697,7 +774,124 @@ RunStats Engine::run_impl(int64_t steps) {
     st.chunks = 1;
   } else {
     st.path = opt_.naive ? "naive" : "stream";
-    if (has_exchange_ && concurrent_ && !opt_.naive) {
+    if (has_exchange_ && sig_mode_ > 0) {
+      // Signalled pipeline (per chunk c), two streams:
+      //   compute: ONE launch of every unit of chunk c, halo-dependent units first (they are
+      //            dispatched first and are short); each of them waits in the kernel until
+      //            halo(c) has landed (halo_counter_), and when done releases its rows at
+      //            system scope and bumps sig_counter_
+      //   comm   : gate (sig_counter_ >= units launched so far) -> halo exchange of chunk c+1
+      //            -> halo_counter_ = c+1
+      // The exchange starts while the interior units of chunk c are still running, no unit
+      // competes with a second stencil launch for wave slots, and the compute stream never
+      // waits on the comm stream (a cross-queue wait costs ~6 us of dispatch latency; with
+      // device_halo_wait = 0 the launch waits on an event instead).
+      bool check = false;
+      int k = next_chunk(steps_done_, target, &check);
+      if (k > 0) {
+        H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
+        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+        trace_begin("exchange", comm_);
+        do_exchange_async(k);
+        trace_end("exchange", comm_);
+        exchange_landed();
+        ++st.exchanges;
+      }
+      while (k > 0) {
+        if (!dev_wait_) H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+        trace_begin("chunk", compute_);
+        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 3);
+        trace_end("chunk", compute_);
+        for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
+        ++st.chunks;
+        bool check_next = false;
+        const int k_next = next_chunk(steps_done_ + k, target, &check_next);
+        if (check) {
+          // nothing is in flight on the comm stream here (the exchange of chunk c completed
+          // before the chunk started), so the all-reduce is the communicator's only operation
+          st.residual = finish_residual();
+          if (st.residual < opt_.sensitivity) {
+            rollback();
+            st.converged = true;
+            break;
+          }
+        }
+        if (k_next > 0) {
+          gate_exchange();
+          trace_begin("exchange", comm_);
+          do_exchange_async(k_next);
+          trace_end("exchange", comm_);
+          exchange_landed();
+          ++st.exchanges;
+        }
+        steps_done_ += k;
+        k = k_next;
+        check = check_next;
+      }
+      H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
+      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
+    } else if (has_exchange_ && concurrent_ && !opt_.naive && opt_.comm_boundary != 0) {
+      // Two-stream concurrent pipeline (per chunk c):
+      //   compute (I): wait evB[c-1] -> interior units(c) -> evI[c]
+      //   comm    (C): wait evI[c-1] -> boundary units(c) -> evB[c] -> halo exchange of chunk c+1
+      // The boundary units and the exchange that consumes their outputs share one stream, so
+      // the boundary -> exchange -> boundary cycle has no cross-queue wait in it (each
+      // cross-queue hand-off costs ~10-20 us of dispatch latency on gfx950, measured in
+      // profiles/overlap_trace_*.txt).  The interior is enqueued first so that a host-side
+      // RCCL enqueue stall never delays it.
+      bool check = false;
+      int k = next_chunk(steps_done_, target, &check);
+      H2D_HIP_CHECK(hipEventRecord(ev_i_[1], compute_));
+      H2D_HIP_CHECK(hipEventRecord(ev_b_[1], compute_));
+      if (k > 0) {
+        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_i_[1], 0));
+        trace_begin("exchange", comm_);
+        do_exchange_async(k);
+        trace_end("exchange", comm_);
+        ++st.exchanges;
+      }
+      int c = 0;
+      while (k > 0) {
+        const int p = c & 1, q = p ^ 1;
+        const int src = tiles_[0].cur;
+        H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[q], 0));
+        trace_begin("interior", compute_);
+        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1, src, compute_);
+        trace_end("interior", compute_);
+        H2D_HIP_CHECK(hipEventRecord(ev_i_[p], compute_));
+        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_i_[q], 0));
+        trace_begin("boundary", comm_);
+        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2, src, comm_);
+        trace_end("boundary", comm_);
+        H2D_HIP_CHECK(hipEventRecord(ev_b_[p], comm_));
+        for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
+        ++st.chunks;
+        bool check_next = false;
+        const int k_next = next_chunk(steps_done_ + k, target, &check_next);
+        if (check) {
+          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[p], 0));
+          for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
+          st.residual = finish_residual();
+          if (st.residual < opt_.sensitivity) {
+            rollback();
+            st.converged = true;
+            break;
+          }
+        }
+        if (k_next > 0) {
+          trace_begin("exchange", comm_);
+          do_exchange_async(k_next);
+          trace_end("exchange", comm_);
+          ++st.exchanges;
+        }
+        steps_done_ += k;
+        k = k_next;
+        check = check_next;
+        ++c;
+      }
+      H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
+      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
+    } else if (has_exchange_ && concurrent_ && !opt_.naive) {
       // Concurrent pipeline (per chunk c), three streams:
       //   B (bstream_): wait halo(c), interior(c-1) -> boundary units(c) -> evB[c&1]
       //   C (comm_)   : wait evB[c&1] -> halo exchange of chunk c+1 (from boundary outputs)
@@ -849,6 +1043,16 @@ RunStats Engine::run_impl(int64_t steps) {
     H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
   }
   wait_event(ev_t1_);
+  if (d_sig_timeout_) {
+    unsigned int to = 0;
+    H2D_HIP_CHECK(hipMemcpy(&to, d_sig_timeout_, sizeof(to), hipMemcpyDeviceToHost));
+    if (to) {
+      H2D_HIP_CHECK(hipMemset(d_sig_timeout_, 0, sizeof(unsigned int)));
+      throw std::runtime_error(std::string("signalled halo pipeline timed out: ") +
+                               ((to & 1) ? "the exchange gate (boundary units never completed) " : "") +
+                               ((to & 2) ? "the device-side halo wait (the exchange never landed)" : ""));
+    }
+  }
   trace_collect(st);
   float ms = 0.0f;
   H2D_HIP_CHECK(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));

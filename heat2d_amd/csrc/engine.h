@@ -52,6 +52,18 @@ struct EngineOptions {
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   int boundary_rows = 8;      // rows per halo-dependent work unit (overlap mode; at least K)
   int concurrent = -1;        // boundary units on a second stream: -1 auto, 0 never, 1 always
+  // concurrent pipeline shape: boundary units on the comm stream ahead of the exchange they
+  // feed (two streams; default), or on a third stream of their own (0)
+  int comm_boundary = -1;
+  // Signalled pipeline: ONE launch per chunk with the halo-dependent units first; each of them
+  // bumps a counter when its rows are final and the comm stream starts the exchange of the
+  // next chunk as soon as the counter says so (mid-kernel).  -1 auto, 0 off,
+  // 1 gate = hipStreamWaitValue64 on signal memory, 2 gate = a one-wave polling kernel.
+  int signal_exchange = -1;
+  // Signalled pipeline: the halo-dependent units wait for the exchange in the kernel (they
+  // poll a counter the comm stream sets after the exchange), so the compute stream never
+  // waits on the comm stream.  -1 auto (on), 0: the chunk launch waits on an event instead.
+  int device_halo_wait = -1;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
   bool poison = false;        // debug canary: NaN in every cell no valid update may read
@@ -109,6 +121,9 @@ class Engine {
   bool on_gpu() const { return opt_.device >= 0; }
   bool has_exchange() const { return has_exchange_; }
   bool concurrent() const { return concurrent_; }
+  int signal_mode() const { return sig_mode_; }
+  // "none" (no exchange), "signal", "concurrent", "concurrent3", "boundary-first", "serial"
+  std::string pipeline() const;
   int rows_per_wave(int K) const;  // largest unit height for depth K (tile 0)
   int num_units(int K) const;      // work units (waves) per chunk of depth K, all tiles
   int64_t steps_done() const { return steps_done_; }
@@ -159,11 +174,13 @@ class Engine {
     Unit* d_all = nullptr;
     Unit* d_interior = nullptr;
     Unit* d_boundary = nullptr;
+    Unit* d_bfirst = nullptr;  // boundary units, then interior units (signalled pipeline)
     int n_all = 0, n_interior = 0, n_boundary = 0;
   };
 
   const UnitLists& units(int t, int K);
-  // which: 0 all, 1 interior, 2 boundary; src: storage index read (-1: current)
+  // which: 0 all, 1 interior, 2 boundary, 3 all boundary-first + signal; src: storage index
+  // read (-1: current)
   void launch_chunk_tile(int t, int K, bool residual, int which, int src = -1, hipStream_t stream = nullptr);
   void reduce_tile_residual(int t, int K);
   void do_exchange_async(int K);  // enqueue on comm stream
@@ -208,6 +225,15 @@ class Engine {
   int64_t stage_cap_ = 0;
   int comm_cus_ = 0, device_cus_ = 0;
   bool contig_ = false;
+  int sig_mode_ = 0;                        // resolved signal_exchange
+  unsigned long long* sig_counter_ = nullptr;  // boundary units completed (cumulative)
+  unsigned long long sig_target_ = 0;          // boundary units launched (cumulative, host)
+  unsigned int* d_sig_timeout_ = nullptr;
+  bool dev_wait_ = false;                      // resolved device_halo_wait
+  unsigned long long* halo_counter_ = nullptr;  // exchanges landed (cumulative)
+  unsigned long long halo_seq_ = 0;            // exchanges enqueued (cumulative, host)
+  void exchange_landed();                   // comm stream: publish halo_seq_ (or record evHalo)
+  void gate_exchange();                     // comm stream: wait until sig_counter_ >= sig_target_
   void* rccl_comm_ = nullptr;       // ncclComm_t
   int rccl_rank_ = 0, rccl_nranks_ = 1;
 };

@@ -66,6 +66,20 @@ struct StreamArgs {
   int per_x, per_y;
   double* partials;  // per-unit residual partial sums (only read by the RESID variant)
   float* dummy;      // >= 256 floats: store target of non-output lanes in the branch-free path
+  // Residual partial of unit w goes to slot (w + prot) mod nunits (a boundary-first list keeps
+  // the interior-then-boundary summation order of the split launches).
+  int prot = 0;
+  // Signalled halo pipeline: units [0, nsignal) release their stores at system scope and add
+  // 1 to *signal when done, so the comm stream can start the exchange mid-kernel.
+  int nsignal = 0;
+  unsigned long long* signal = nullptr;
+  // Device-side halo wait: units [0, nsignal) first poll *halo_ready until it reaches
+  // halo_need (the exchange that fills their ghost rows has landed); after halo_polls polls
+  // they give up and set bit 2 of *timed_out.
+  const unsigned long long* halo_ready = nullptr;
+  unsigned long long halo_need = 0;
+  long long halo_polls = 0;
+  unsigned int* timed_out = nullptr;
 };
 
 // Largest K with a compiled streaming kernel.
@@ -79,6 +93,12 @@ void launch_init(const TileGeom& g, float* base, int init, hipStream_t s);
 void launch_poison(const TileGeom& g, float* base, bool fixed, bool per_x, bool per_y, hipStream_t s);
 void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s);
 void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s);
+// One wave polls *counter (system-scope acquire loads, s_sleep between polls) until it reaches
+// `target`; after `max_polls` it gives up and sets *timed_out (the caller reports it).
+void launch_wait_counter(const unsigned long long* counter, unsigned long long target, unsigned int* timed_out,
+                         long long max_polls, hipStream_t s);
+// *counter = value with a system-scope release, once every earlier command on `s` is done.
+void launch_set_counter(unsigned long long* counter, unsigned long long value, hipStream_t s);
 // Residual of a whole tile (Σ (a-b)² over owned cells) — used by tests/ops.
 void launch_tile_residual(const TileGeom& g, const float* a, const float* b, double* partials, int npartials,
                           hipStream_t s);

@@ -68,6 +68,23 @@ __global__ __launch_bounds__(256) void reduce_sum_kernel(const double* __restric
   if (threadIdx.x == 0) *out = ((part[0] + part[1]) + part[2]) + part[3];
 }
 
+// Comm-stream gate of the signalled halo pipeline (see Engine::run_impl): one lane polls the
+// boundary-unit counter with system-scope acquire loads.  Bounded: a gate that never opens
+// reports a timeout instead of hanging the queue.
+__global__ __launch_bounds__(64) void wait_counter_kernel(const unsigned long long* counter, unsigned long long target,
+                                                          unsigned int* timed_out, long long max_polls) {
+  if (threadIdx.x != 0) return;
+  for (long long i = 0; i < max_polls; ++i) {
+    if (__hip_atomic_load(counter, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= target) return;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  __hip_atomic_fetch_or(timed_out, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void set_counter_kernel(unsigned long long* counter, unsigned long long value) {
+  if (threadIdx.x == 0) __hip_atomic_store(counter, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(256) void tile_residual_kernel(TileGeom g, const float* __restrict__ a,
                                                              const float* __restrict__ b, double* __restrict__ partials) {
   __shared__ double part[4];
@@ -409,6 +426,17 @@ void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hi
 
 void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s) {
   hipLaunchKernelGGL(reduce_sum_kernel, dim3(1), dim3(256), 0, s, in, n, out);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_wait_counter(const unsigned long long* counter, unsigned long long target, unsigned int* timed_out,
+                         long long max_polls, hipStream_t s) {
+  hipLaunchKernelGGL(wait_counter_kernel, dim3(1), dim3(64), 0, s, counter, target, timed_out, max_polls);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_set_counter(unsigned long long* counter, unsigned long long value, hipStream_t s) {
+  hipLaunchKernelGGL(set_counter_kernel, dim3(1), dim3(64), 0, s, counter, value);
   H2D_HIP_CHECK(hipGetLastError());
 }
 

@@ -225,6 +225,20 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const int w = (int)blockIdx.x * 4 + wv;
   if (w >= a.nunits) return;
   const int lane = (int)(threadIdx.x & 63);
+  if (a.halo_ready != nullptr && w < a.nsignal) {
+    // halo-dependent unit: wait until the exchange that fills its ghost rows has landed
+    if (lane == 0) {
+      long long i = 0;
+      while (__hip_atomic_load(a.halo_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.halo_need) {
+        if (++i > a.halo_polls) {
+          __hip_atomic_fetch_or(a.timed_out, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
   const Unit u = a.units[w];
   const int64_t y0 = (int64_t)u.strip * a.wout;
   const int64_t x0 = u.x0;
@@ -267,7 +281,15 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   }
   if constexpr (RESID) {
     racc = wave_sum(racc);
-    if (lane == 0) a.partials[w] = racc;
+    int slot = w + a.prot;
+    if (slot >= a.nunits) slot -= a.nunits;
+    if (lane == 0) a.partials[slot] = racc;
+  }
+  if (a.signal != nullptr && w < a.nsignal) {
+    // halo rows of this unit are final: make them visible device- and system-wide (the
+    // exchange may read them from another queue or over xGMI), then count the unit
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_fetch_add(a.signal, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

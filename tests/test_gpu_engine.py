@@ -163,16 +163,27 @@ def test_rccl_convergence_allreduce(native, gpu):
     assert np.array_equal(eng.download(0), ref["grid"])
 
 
+# pipeline: 0 boundary-first (one stream), 1 concurrent with the boundary units on the comm
+# stream (two streams), 2 concurrent with a boundary stream of its own (three streams),
+# 3 signalled (one launch per chunk, exchange gated mid-kernel by hipStreamWaitValue64),
+# 4 signalled with a polling-kernel gate (the default), 5 the same with the chunk launch waiting on
+# a halo event instead of the in-kernel halo wait
+PIPELINES = {0: dict(concurrent=0, signal_exchange=0), 1: dict(concurrent=1, signal_exchange=0),
+             2: dict(concurrent=1, comm_boundary=0, signal_exchange=0), 3: dict(signal_exchange=1),
+             4: dict(signal_exchange=2), 5: dict(signal_exchange=2, device_halo_wait=0)}
+PIPELINE_NAMES = {0: "boundary-first", 1: "concurrent", 2: "concurrent3", 3: "signal", 4: "signal", 5: "signal"}
+
+
 @pytest.mark.parametrize("gx,gy", [(2, 1), (4, 1), (2, 2), (1, 3)])
-@pytest.mark.parametrize("concurrent", [0, 1])
-def test_overlap_pipelines(native, gpu, gx, gy, concurrent):
-    """Boundary-first (single stream) and concurrent (two streams) pipelines, with convergence."""
+@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5])
+def test_overlap_pipelines(native, gpu, gx, gy, pipeline):
+    """Boundary-first and concurrent pipelines, with convergence."""
     nx, ny, steps = 257, 509, 45
     kw = dict(convergence=True, interval=9, sensitivity=1e-30)
     for boundary in (0, 1):
         eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=boundary, tblock=8, device=gpu,
-                            concurrent=concurrent, **kw)
-        assert eng.concurrent() == bool(concurrent)
+                            **PIPELINES[pipeline], **kw)
+        assert eng.pipeline() == PIPELINE_NAMES[pipeline]
         st = eng.run(steps)
         assert st["steps_done"] == steps
         ref = oracle(native, nx, ny, steps, boundary, **kw)
@@ -180,24 +191,26 @@ def test_overlap_pipelines(native, gpu, gx, gy, concurrent):
         for t in range(eng.num_tiles()):
             g = eng.geom(t)
             out[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]] = eng.download(t)
-        assert np.array_equal(out, ref["grid"]), (gx, gy, boundary, concurrent)
+        assert np.array_equal(out, ref["grid"]), (gx, gy, boundary, pipeline)
 
 
-def test_concurrent_auto_for_row_strips(native, gpu):
-    eng = native.Engine(2048, 2048, gridx=4, gridy=1, device=gpu)
-    assert eng.concurrent()
+def test_pipeline_auto(native, gpu):
+    assert native.Engine(2048, 2048, gridx=4, gridy=1, device=gpu).pipeline() == "signal"
+    assert native.Engine(2048, 2048, gridx=4, gridy=1, device=gpu, signal_exchange=0).pipeline() == "concurrent"
+    assert native.Engine(2048, 2048, gridx=2, gridy=2, device=gpu, overlap=False).pipeline() == "serial"
+    assert native.Engine(2048, 2048, device=gpu).pipeline() == "none"
 
 
-@pytest.mark.parametrize("concurrent", [0, 1])
+@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("contig,comm_cus", [(0, 0), (1, 0), (1, 8), (0, 4)])
 @pytest.mark.parametrize("boundary", [0, 1])
-def test_rccl_self_exchange_row_periodic(native, gpu, concurrent, contig, comm_cus, boundary):
+def test_rccl_self_exchange_row_periodic(native, gpu, pipeline, contig, comm_cus, boundary):
     """Row-periodic single rank: the per-rank shape of the 1-D row-strip bench.  Covers the
     contiguous K-row halo path (no pack/unpack) and CU-partitioned comm/compute streams."""
     nx, ny, steps = 300, 701, 37
     eng = native.Engine(nx, ny, periodic_x=True, boundary=boundary, device=gpu, ranks=[0],
-                        transport=native.TRANSPORT_RCCL, concurrent=concurrent, contiguous_halo=contig,
-                        comm_cus=comm_cus, poison=True)
+                        transport=native.TRANSPORT_RCCL, contiguous_halo=contig,
+                        comm_cus=comm_cus, poison=True, **PIPELINES[pipeline])
     assert eng.contiguous_halo() == bool(contig) and eng.comm_cus() == comm_cus
     eng.init_rccl(native.Engine.rccl_unique_id(), 1, 0)
     eng.run(steps)
