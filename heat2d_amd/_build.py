@@ -35,6 +35,7 @@ RUNTIME_SOURCES = [
     "io.cpp",
     "engine.cpp",
     "kernels.hip",
+    "tile_kernel.hip",
 ] + [f"stream_k{k}.hip" for k in (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16)]
 EXT_SOURCES = RUNTIME_SOURCES + ["bindings.cpp"]
 CLI_SOURCES = RUNTIME_SOURCES + ["heat2d_main.cpp"]

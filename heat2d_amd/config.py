@@ -47,6 +47,7 @@ class Config:
     rows_per_wave: int = 0
     overlap: bool = True
     small_grid: bool = True
+    tiled: str = "auto"  # auto | on | off: LDS-tiled temporally-blocked kernel (single-tile small/medium grids)
     naive: bool = False
     tune: bool = False  # autotune K / rows-per-wave on scratch engines before the run (single GPU)
     json: bool = False
@@ -126,6 +127,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--rows-per-wave", type=int, default=0, help="rows per wave work unit (0 = auto)")
     p.add_argument("--no-overlap", action="store_true", help="do not overlap halo exchange with interior compute")
     p.add_argument("--no-small-grid", action="store_true", help="disable the whole-grid LDS solver")
+    p.add_argument("--tiled", choices=("auto", "on", "off"), default="auto",
+                   help="LDS-tiled temporally-blocked kernel for single-tile small/medium grids")
     p.add_argument("--naive", action="store_true", help="validation kernel: one thread per cell, one step per launch")
     p.add_argument("--tune", action="store_true", help="autotune the temporal block / unit size before the run")
     p.add_argument("--json", action="store_true", help="print a JSON metrics line")
@@ -171,6 +174,7 @@ def config_from_args(argv: Optional[Sequence[str]] = None) -> Config:
         rows_per_wave=a.rows_per_wave,
         overlap=not a.no_overlap,
         small_grid=not a.no_small_grid,
+        tiled=a.tiled,
         naive=a.naive,
         tune=a.tune,
         json=a.json,

@@ -260,7 +260,7 @@ PYBIND11_MODULE(_heat2d, m) {
                        int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
                        bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s, bool trace, bool poison,
                        int comm_cus, int contiguous_halo, int comm_cu_layout, int reserve_waves,
-                       bool device_fence_events, int comm_boundary, int signal_exchange, int device_halo_wait) {
+                       bool device_fence_events, int comm_boundary, int signal_exchange, int device_halo_wait, int tiled, int tile_rows, int tile_width, int tile_k) {
              EngineOptions o;
              o.nx = nx;
              o.ny = ny;
@@ -299,6 +299,10 @@ PYBIND11_MODULE(_heat2d, m) {
              o.comm_boundary = comm_boundary;
              o.signal_exchange = signal_exchange;
              o.device_halo_wait = device_halo_wait;
+             o.tiled = tiled;
+             o.tile_rows = tile_rows;
+             o.tile_width = tile_width;
+             o.tile_k = tile_k;
              return new Engine(o);
            }),
            py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
@@ -311,7 +315,8 @@ PYBIND11_MODULE(_heat2d, m) {
            py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0, py::arg("concurrent") = -1, py::arg("boundary_rows") = 8,
            py::arg("watchdog_s") = 900.0, py::arg("trace") = false, py::arg("poison") = false,
            py::arg("comm_cus") = -1, py::arg("contiguous_halo") = -1, py::arg("comm_cu_layout") = 0, py::arg("reserve_waves") = -1,
-           py::arg("device_fence_events") = false, py::arg("comm_boundary") = -1, py::arg("signal_exchange") = -1, py::arg("device_halo_wait") = -1)
+           py::arg("device_fence_events") = false, py::arg("comm_boundary") = -1, py::arg("signal_exchange") = -1, py::arg("device_halo_wait") = -1,
+           py::arg("tiled") = -1, py::arg("tile_rows") = 0, py::arg("tile_width") = 0, py::arg("tile_k") = 0)
       .def("num_tiles", &Engine::num_tiles)
       .def("tile_rank", &Engine::tile_rank)
       .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })
@@ -320,6 +325,8 @@ PYBIND11_MODULE(_heat2d, m) {
       .def("concurrent", &Engine::concurrent)
       .def("signal_mode", &Engine::signal_mode)
       .def("pipeline", &Engine::pipeline)
+      .def("tiled", &Engine::tiled)
+      .def("tile_config", &Engine::tile_config)
       .def("comm_cus", &Engine::comm_cus)
       .def("contiguous_halo", &Engine::contiguous_halo)
       .def("wave_capacity", &Engine::wave_capacity)

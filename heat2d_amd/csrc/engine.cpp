@@ -249,6 +249,40 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     for (int t = 0; t < (int)tiles_.size(); ++t)
       for (int K = 1; K <= G_; ++K)
         if (stream_k_supported(K)) units(t, K);
+    // LDS-tiled path: one tile owning the whole grid (any periodic halo is its own wrap).
+    const bool self_only = tiles_.size() == 1 && transport_ == kTransportLocal;
+    if (self_only && !opt_.naive && opt_.tiled != 0) {
+      const int64_t NX = dec_.NX, NY = dec_.NY;
+      // Auto: the tiled path up to 640x512-class grids; the whole-grid LDS solver keeps
+      // convergence runs that fit it (its check needs no host round trip).  Measured on
+      // MI355X, ref precision, 1000 steps (profiles/tile_sweep_r1.txt), us/step
+      // tiled / LDS solver / streaming: 80x64 0.90 / 1.56 / 1.60; 160x128 0.87 / 4.05 / 1.63;
+      // 320x256 0.91 / - / 1.61; 640x512 1.36 / - / 1.89; 1280x1024 2.50 / - / 2.07.
+      const int64_t cells = NX * NY;
+      const bool lds_whole = opt_.small_grid_lds && !has_exchange_ && lds_solver_fits(NX, NY) && opt_.convergence;
+      const bool want = opt_.tiled == 1 || (cells <= 600000 && !lds_whole);
+      if (want && NX < (1 << 30) && NY < (1 << 30)) {
+        int RY = opt_.tile_width > 0 ? opt_.tile_width : 64;
+        if (RY != 64 && RY != 128) throw std::invalid_argument("tile_width must be 64 or 128");
+        int K = opt_.tile_k > 0 ? opt_.tile_k : (cells <= 32768 ? 16 : 8);
+        K = std::max(1, std::min(K, (RY - 4) / 2));
+        int TX = opt_.tile_rows;
+        if (TX <= 0) TX = cells <= 131072 ? 8 : 16;
+        while (TX > 1 && !tile_config_ok(TX, RY, K)) TX /= 2;
+        if (!tile_config_ok(TX, RY, K)) throw std::invalid_argument("no valid LDS tile configuration");
+        tiled_ = true;
+        tile_tx_ = TX;
+        tile_ry_ = RY;
+        tile_k_ = K;
+        Tile& T = tiles_[0];
+        const int64_t need = tile_count((int)NX, (int)NY, TX, RY - 2 * K);
+        if (need > T.pcap) {
+          hipFree(T.partials);
+          T.pcap = need;
+          T.partials = dmalloc<double>((size_t)need);
+        }
+      }
+    }
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
   }
 }
@@ -433,11 +467,13 @@ void Engine::reduce_tile_residual(int t, int K) {
   launch_reduce_sum(tiles_[t].partials, L.n_all, d_resid_ + t, compute_);
 }
 
-int Engine::next_chunk(int64_t done, int64_t total, bool* check) const {
+int Engine::chunk_len(int64_t done, int64_t total, int kmax, bool* check) const {
+  // A chunk never crosses a convergence check; the check step is a chunk of its own, so a
+  // converged run can roll back exactly one step (B-5 semantics).
   *check = false;
   const int64_t remaining = total - done;
   if (remaining <= 0) return 0;
-  int64_t k = std::min<int64_t>(G_, remaining);
+  int64_t k = std::min<int64_t>(kmax, remaining);
   if (opt_.convergence) {
     const int64_t next_check = (done / opt_.interval + 1) * opt_.interval;
     if (done + 1 == next_check) {
@@ -446,6 +482,12 @@ int Engine::next_chunk(int64_t done, int64_t total, bool* check) const {
     }
     k = std::min<int64_t>(k, next_check - 1 - done);
   }
+  return (int)std::max<int64_t>(1, k);
+}
+
+int Engine::next_chunk(int64_t done, int64_t total, bool* check) const {
+  int64_t k = chunk_len(done, total, G_, check);
+  if (k == 0) return 0;
   if (on_gpu() && !opt_.naive)
     while (k > 1 && !stream_k_supported((int)k)) --k;
   if (opt_.naive) k = 1;
@@ -751,7 +793,48 @@ RunStats Engine::run_impl(int64_t steps) {
 
   H2D_HIP_CHECK(hipEventRecord(ev_t0_, compute_));
   const bool single = tiles_.size() == 1 && !has_exchange_;
-  if (single && opt_.small_grid_lds && !opt_.naive && lds_solver_fits(dec_.NX, dec_.NY) && steps > 0) {
+  if (tiled_) {
+    // LDS-tiled path: one launch per chunk of up to tile_k_ steps, the tiling re-derived per
+    // chunk length (TY = RY - 2k).
+    st.path = "tiled";
+    Tile& T = tiles_[0];
+    while (steps_done_ < target) {
+      bool check = false;
+      const int k = chunk_len(steps_done_, target, tile_k_, &check);
+      TileArgs a;
+      a.src = T.buf[T.cur] + T.g.idx(0, 0);
+      a.dst = T.buf[1 - T.cur] + T.g.idx(0, 0);
+      a.pitch = T.g.pitch;
+      a.NX = (int)T.g.xcell;
+      a.NY = (int)T.g.ycell;
+      a.TX = tile_tx_;
+      a.RY = tile_ry_;
+      a.K = k;
+      a.TY = tile_ry_ - 2 * k;
+      a.cx = opt_.cx;
+      a.cy = opt_.cy;
+      a.fixed = opt_.boundary == kFixed;
+      a.per_x = opt_.periodic_x;
+      a.per_y = opt_.periodic_y;
+      a.partials = T.partials;
+      trace_begin("step", compute_);
+      launch_tile(a, opt_.precision, check, compute_);
+      trace_end("step", compute_);
+      if (check) launch_reduce_sum(T.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
+      T.cur = 1 - T.cur;
+      ++st.chunks;
+      if (check) {
+        st.residual = finish_residual();
+        if (st.residual < opt_.sensitivity) {
+          rollback();
+          st.converged = true;
+          break;
+        }
+      }
+      steps_done_ += k;
+    }
+    H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
+  } else if (single && opt_.small_grid_lds && !opt_.naive && lds_solver_fits(dec_.NX, dec_.NY) && steps > 0) {
     // Whole run inside one workgroup's LDS.
     st.path = "lds";
     Tile& T = tiles_[0];

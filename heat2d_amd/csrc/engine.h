@@ -28,6 +28,7 @@
 #include "cpu_reference.h"
 #include "decomposition.h"
 #include "kernels.h"
+#include "tile_kernel.h"
 
 namespace h2d {
 
@@ -75,6 +76,11 @@ struct EngineOptions {
   int transport = kTransportAuto;
   bool overlap = true;     // overlap halo exchange with interior compute
   bool small_grid_lds = true;  // whole-grid LDS solver for small single-tile problems
+  // LDS-tiled temporally-blocked kernel (tile_kernel.hip) for single-tile runs of small and
+  // medium grids: -1 auto (by size), 0 off, 1 on.  tile_rows = TX, tile_width = RY (64 or
+  // 128 region columns), tile_k = steps per launch; 0 = automatic.
+  int tiled = -1;
+  int tile_rows = 0, tile_width = 0, tile_k = 0;
   bool naive = false;      // validation: one-thread-per-cell single-step kernel
   // CUs reserved for the comm stream (pack/unpack/RCCL kernels) when halos are exchanged;
   // the compute streams are masked to the other CUs so the exchange kernels never wait for
@@ -122,6 +128,8 @@ class Engine {
   bool has_exchange() const { return has_exchange_; }
   bool concurrent() const { return concurrent_; }
   int signal_mode() const { return sig_mode_; }
+  bool tiled() const { return tiled_; }
+  std::vector<int> tile_config() const { return {tile_tx_, tile_ry_, tile_k_}; }
   // "none" (no exchange), "signal", "concurrent", "concurrent3", "boundary-first", "serial"
   std::string pipeline() const;
   int rows_per_wave(int K) const;  // largest unit height for depth K (tile 0)
@@ -186,6 +194,7 @@ class Engine {
   void do_exchange_async(int K);  // enqueue on comm stream
   double finish_residual();       // reduce + (rccl) all-reduce, host sync
   void wait_event(hipEvent_t ev);  // blocking wait with RCCL error polling + watchdog
+  int chunk_len(int64_t done, int64_t total, int kmax, bool* check) const;  // convergence-aligned chunk
   RunStats run_impl(int64_t steps);
   CopyDesc* local_descs(int K, int& n, int64_t& maxe);
   void check_tile(int t) const;
@@ -225,6 +234,8 @@ class Engine {
   int64_t stage_cap_ = 0;
   int comm_cus_ = 0, device_cus_ = 0;
   bool contig_ = false;
+  bool tiled_ = false;                      // resolved EngineOptions::tiled
+  int tile_tx_ = 0, tile_ry_ = 0, tile_k_ = 0;
   int sig_mode_ = 0;                        // resolved signal_exchange
   unsigned long long* sig_counter_ = nullptr;  // boundary units completed (cumulative)
   unsigned long long sig_target_ = 0;          // boundary units launched (cumulative, host)

@@ -1,0 +1,26 @@
+// heat2d_amd — launch interface of the LDS-tiled temporally-blocked kernel (tile_kernel.hip).
+#pragma once
+
+#include "kernels.h"
+
+namespace h2d {
+
+// Arguments of the LDS-tiled temporally-blocked kernel (tile_kernel.hip): one 256-thread
+// workgroup per TX x TY tile, K steps per launch, region RY = TY + 2K columns (64 or 128).
+struct TileArgs {
+  const float* src;  // owned cell (0, 0) of the single tile (whole grid)
+  float* dst;
+  int64_t pitch;
+  int NX, NY;
+  int TX, TY, RY, K;
+  int tiles_y = 0, ntiles = 0;  // set by launch_tile
+  double cx, cy;
+  int fixed, per_x, per_y;
+  double* partials;  // [ntiles] residual partials (residual launches)
+};
+size_t tile_lds_bytes(int TX, int RY, int K);
+bool tile_config_ok(int TX, int RY, int K);
+int tile_count(int NX, int NY, int TX, int TY);
+void launch_tile(TileArgs a, int precision, bool residual, hipStream_t s);
+
+}  // namespace h2d

@@ -1,0 +1,181 @@
+// heat2d_amd — LDS-tiled, temporally-blocked stencil for small and medium grids (gfx950).
+//
+// The streaming kernel (stream_kernel.hpp) parallelises over 256-column strips and walks
+// rows; on grids of 10^4..10^6 cells (the reference's whole measured table, Report.pdf p.21,
+// p.26: 80x64 .. 1280x1024) that leaves most of the 1024 SIMDs idle or the waves latency
+// bound.  This kernel parallelises over 2-D tiles instead:
+//   * one 256-thread workgroup owns a TX x TY tile; it loads the tile plus a k-deep halo
+//     (region (TX+2k) x RY, RY = TY+2k = 64 or 128 columns) into LDS once per launch;
+//   * it advances k time steps inside LDS (ping-pong buffers, one barrier per step),
+//     recomputing the halo redundantly (overlapped tiling: no inter-workgroup exchange);
+//   * each thread owns a fixed 4-column group (float4 LDS traffic, 2 scalar side reads) and
+//     strides over rows; cells outside the shrinking valid region are computed on stale data
+//     but never feed a valid cell (dependency cone), so no per-cell range test is needed;
+//   * global edges: fixed edges hold, the ghost-zero ring stays 0, periodic dims wrap on load;
+//   * the owned tile is written back once per k steps; one launch per chunk (~1.5 us kernel
+//     boundary on gfx950, cheaper than any in-kernel grid barrier).
+// The tile -> workgroup map keeps neighbouring tiles on one XCD (blocks are dealt round-robin
+// over the 8 XCDs) so their shared halo rows hit the same L2.
+// Numerics: the same cell() as the streaming kernel (bit-exact ref path / fp32 FMA path).
+// Compiled with -ffp-contract=off.
+#include "stream_kernel.hpp"
+#include "tile_kernel.h"
+
+namespace h2d {
+namespace {
+
+__device__ __forceinline__ int wrap_idx(int i, int n) {
+  i %= n;
+  return i < 0 ? i + n : i;
+}
+
+template <bool F32, bool RESID, int RY>
+__global__ __launch_bounds__(256) void tile_lds_kernel(TileArgs a) {
+  extern __shared__ float4 lds4[];
+  float* lds = reinterpret_cast<float*>(lds4);
+  constexpr int G4 = RY / 4;          // float4 column groups per region row
+  constexpr int W = RY + 8;           // LDS row: 4 pad | RY region columns | 4 pad
+  constexpr int RSTEP = 256 / G4;     // rows per sweep of the workgroup
+  const int tid = threadIdx.x;
+  const int K = a.K;
+  const int RX = a.TX + 2 * K;
+  // XCD-aware tile order: block b runs on XCD b % 8; give each XCD a contiguous tile range
+  int b = blockIdx.x;
+  if (a.ntiles % 8 == 0) b = (b & 7) * (a.ntiles >> 3) + (b >> 3);
+  const int bx = b / a.tiles_y, by = b - bx * a.tiles_y;
+  const int x0 = bx * a.TX - K;  // global row of region row 0
+  const int y0 = by * a.TY - K;  // global column of region column 0
+  float* cur = lds;
+  float* nxt = lds + RX * W;
+
+  // ---- load the region (zero outside a non-periodic grid) ----
+  for (int e = tid; e < RX * RY; e += 256) {
+    const int r = e / RY, c = e - r * RY;
+    int gr = x0 + r, gc = y0 + c;
+    bool in = true;
+    if (a.per_x) gr = wrap_idx(gr, a.NX);
+    else in = gr >= 0 && gr < a.NX;
+    if (a.per_y) gc = wrap_idx(gc, a.NY);
+    else in = in && gc >= 0 && gc < a.NY;
+    cur[r * W + 4 + c] = in ? a.src[(int64_t)gr * a.pitch + gc] : 0.0f;
+  }
+
+  // ---- per-thread column group and its edge masks (fixed: hold, ghost-zero: zero) ----
+  const int q = tid % G4;
+  const int r_off = tid / G4;
+  const int gc0 = y0 + 4 * q;
+  unsigned cmask = 0;
+  if (!a.per_y) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gc = gc0 + j;
+      const bool m = a.fixed ? (gc == 0 || gc == a.NY - 1) : (gc < 0 || gc >= a.NY);
+      cmask |= (m ? 1u : 0u) << j;
+    }
+  }
+  // residual: owned, in-grid columns of this group
+  unsigned own = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 4 * q + j;
+    const bool o = c >= K && c < K + a.TY && (by * a.TY + (c - K)) < a.NY;
+    own |= (o ? 1u : 0u) << j;
+  }
+  const Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
+  double racc = 0.0;
+  __syncthreads();
+
+  for (int t = 1; t <= K; ++t) {
+    const bool last = t == K;
+    for (int r = t + r_off; r < RX - t; r += RSTEP) {
+      const float* p = cur + r * W + 4 + 4 * q;
+      const float4 C = *reinterpret_cast<const float4*>(p);
+      const float4 N = *reinterpret_cast<const float4*>(p - W);
+      const float4 S = *reinterpret_cast<const float4*>(p + W);
+      const float wv = p[-1], ev = p[4];
+      float4 o;
+      o.x = cell<F32>(C.x, N.x, S.x, wv, C.y, k);
+      o.y = cell<F32>(C.y, N.y, S.y, C.x, C.z, k);
+      o.z = cell<F32>(C.z, N.z, S.z, C.y, C.w, k);
+      o.w = cell<F32>(C.w, N.w, S.w, C.z, ev, k);
+      const int gr = x0 + r;
+      bool rm = false;
+      if (!a.per_x) rm = a.fixed ? (gr == 0 || gr == a.NX - 1) : (gr < 0 || gr >= a.NX);
+      const unsigned m = rm ? 0xFu : cmask;
+      if (a.fixed) {
+        o.x = (m & 1u) ? C.x : o.x;
+        o.y = (m & 2u) ? C.y : o.y;
+        o.z = (m & 4u) ? C.z : o.z;
+        o.w = (m & 8u) ? C.w : o.w;
+      } else {
+        o.x = (m & 1u) ? 0.0f : o.x;
+        o.y = (m & 2u) ? 0.0f : o.y;
+        o.z = (m & 4u) ? 0.0f : o.z;
+        o.w = (m & 8u) ? 0.0f : o.w;
+      }
+      *reinterpret_cast<float4*>(nxt + r * W + 4 + 4 * q) = o;
+      if constexpr (RESID) {
+        if (last && r >= K && r < K + a.TX && bx * a.TX + (r - K) < a.NX) {
+          racc += (own & 1u) ? sq_diff(o.x, C.x) : 0.0;
+          racc += (own & 2u) ? sq_diff(o.y, C.y) : 0.0;
+          racc += (own & 4u) ? sq_diff(o.z, C.z) : 0.0;
+          racc += (own & 8u) ? sq_diff(o.w, C.w) : 0.0;
+        }
+      }
+    }
+    __syncthreads();
+    float* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+
+  // ---- write the owned tile back ----
+  const int xs = bx * a.TX, ys = by * a.TY;
+  for (int e = tid; e < a.TX * a.TY; e += 256) {
+    const int i = e / a.TY, j = e - i * a.TY;
+    if (xs + i < a.NX && ys + j < a.NY) a.dst[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + 4 + K + j];
+  }
+  if constexpr (RESID) {
+    __shared__ double part[4];
+    racc = wave_sum(racc);
+    if ((tid & 63) == 0) part[tid >> 6] = racc;
+    __syncthreads();
+    if (tid == 0) a.partials[blockIdx.x] = ((part[0] + part[1]) + part[2]) + part[3];
+  }
+}
+
+template <bool F32, bool RESID>
+void launch_ry(const TileArgs& a, size_t lds, hipStream_t s) {
+  const dim3 grid((unsigned)a.ntiles), block(256);
+  if (a.RY == 64) hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 64>), grid, block, lds, s, a);
+  else hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 128>), grid, block, lds, s, a);
+}
+
+}  // namespace
+
+size_t tile_lds_bytes(int TX, int RY, int K) { return (size_t)2 * (size_t)(TX + 2 * K) * (size_t)(RY + 8) * sizeof(float); }
+
+bool tile_config_ok(int TX, int RY, int K) {
+  return (RY == 64 || RY == 128) && K >= 1 && RY - 2 * K >= 4 && TX >= 1 && tile_lds_bytes(TX, RY, K) <= 65536;
+}
+
+void launch_tile(TileArgs a, int precision, bool residual, hipStream_t s) {
+  if (!tile_config_ok(a.TX, a.RY, a.K)) throw std::invalid_argument("launch_tile: bad tile configuration");
+  if (a.TY != a.RY - 2 * a.K) throw std::invalid_argument("launch_tile: TY must be RY - 2K");
+  a.tiles_y = (a.NY + a.TY - 1) / a.TY;
+  a.ntiles = ((a.NX + a.TX - 1) / a.TX) * a.tiles_y;
+  const size_t lds = tile_lds_bytes(a.TX, a.RY, a.K);
+  const bool f32 = precision == kFp32;
+  if (f32) {
+    if (residual) launch_ry<true, true>(a, lds, s);
+    else launch_ry<true, false>(a, lds, s);
+  } else {
+    if (residual) launch_ry<false, true>(a, lds, s);
+    else launch_ry<false, false>(a, lds, s);
+  }
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+int tile_count(int NX, int NY, int TX, int TY) { return ((NX + TX - 1) / TX) * ((NY + TY - 1) / TY); }
+
+}  // namespace h2d

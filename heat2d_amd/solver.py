@@ -50,38 +50,44 @@ class RunResult:
 
 
 def autotune(cfg: Config, model, device: int, candidates_k=(2, 4, 8), candidates_h=(0, 4, 8, 16, 32),
+             tile_candidates=((64, 16, 8), (64, 8, 8), (64, 8, 16), (64, 4, 8), (128, 8, 16), (128, 8, 32)),
              trial_steps: int = 0) -> dict:
-    """Pick the temporal-block depth K and rows per wave H for a single-tile GPU run by
-    timing each candidate on a scratch engine (the real field is untouched).  Small and
-    medium grids are latency-bound and prefer short units; large grids keep the defaults."""
+    """Pick the fastest single-tile GPU path by timing candidates on scratch engines (the real
+    field is untouched): the whole-grid LDS solver, the streaming kernel over (K, rows per
+    wave H), and the LDS-tiled kernel over (width RY, steps per launch K, tile rows TX).
+    Returns the engine keyword overrides of the winner (``engine_kw``) and the timing table."""
     n = native()
     cells = cfg.nx * cfg.ny
     steps = trial_steps or max(32, min(256, int(2e8 // max(1, cells))))
-    table = []
-    best = None
+    if cfg.convergence:  # the LDS solver resumes only on a multiple of the check interval
+        steps = -(-steps // cfg.interval) * cfg.interval
+    base = dict(boundary=model.boundary_id(), precision=model.precision_id(), init=model.init_id(), cx=model.cx,
+                cy=model.cy, device=device, convergence=cfg.convergence, interval=cfg.interval,
+                sensitivity=-1.0)  # never converges: every candidate runs the same steps
+    cands = []
     if n.lds_solver_fits(cfg.nx, cfg.ny) and cfg.small_grid:
-        e = n.Engine(cfg.nx, cfg.ny, boundary=model.boundary_id(), precision=model.precision_id(),
-                     init=model.init_id(), cx=model.cx, cy=model.cy, device=device, small_grid_lds=True)
-        e.run(steps)
-        t = min(e.run(steps)["device_ms"] for _ in range(2)) / steps
-        table.append(("lds", 0, t))
-        best = ("lds", 0, t)
+        cands.append(("lds", dict(small_grid_lds=True, tiled=0)))
     for K in candidates_k:
         for H in candidates_h:
-            e = n.Engine(cfg.nx, cfg.ny, boundary=model.boundary_id(), precision=model.precision_id(),
-                         init=model.init_id(), cx=model.cx, cy=model.cy, tblock=K, rows_per_wave=H, device=device,
-                         small_grid_lds=False)
-            e.run(steps)  # warm
-            t = min(e.run(steps)["device_ms"] for _ in range(2)) / steps
-            table.append((K, H, t))
-            if best is None or t < best[2]:
-                best = (K, H, t)
-            del e
-    if best[0] == "lds":
-        return {"tblock": cfg.tblock, "rows_per_wave": 0, "small_grid": True, "us_per_step": best[2] * 1e3,
-                "table": table}
-    return {"tblock": best[0], "rows_per_wave": best[1], "small_grid": False, "us_per_step": best[2] * 1e3,
-            "table": table}
+            cands.append((f"stream K={K} H={H}", dict(tblock=K, rows_per_wave=H, small_grid_lds=False, tiled=0)))
+    if cfg.tiled != "off":
+        for ry, k, tx in tile_candidates:
+            cands.append((f"tiled RY={ry} K={k} TX={tx}",
+                          dict(tiled=1, tile_width=ry, tile_k=k, tile_rows=tx, small_grid_lds=False)))
+    table = []
+    best = None
+    for name, kw in cands:
+        try:
+            e = n.Engine(cfg.nx, cfg.ny, **base, **kw)
+        except Exception:
+            continue
+        e.run(steps)  # warm
+        t = min(e.run(steps)["device_ms"] for _ in range(2)) / steps
+        table.append((name, t * 1e3))
+        if best is None or t < best[2]:
+            best = (name, kw, t)
+        del e
+    return {"choice": best[0], "engine_kw": best[1], "us_per_step": best[2] * 1e3, "table": table}
 
 
 class Solver:
@@ -117,10 +123,10 @@ class Solver:
             self.device = -1
         self.transport = transport
         self.tuned = None
+        self.engine_kw = {}
         if cfg.tune and self.on_gpu and world == 1 and self.nranks == 1:
             self.tuned = autotune(cfg, self.model, self.device)
-            cfg.tblock, cfg.rows_per_wave = self.tuned["tblock"], self.tuned["rows_per_wave"]
-            cfg.small_grid = self.tuned["small_grid"]
+            self.engine_kw = dict(self.tuned["engine_kw"])
         self.engine = self._make_engine(transport, ranks)
         self.exchanger = None
         if transport == n.TRANSPORT_RCCL and self.engine.has_exchange():
@@ -151,13 +157,15 @@ class Solver:
 
     def _make_engine(self, transport: int, ranks):
         cfg, n = self.cfg, native()
+        kw = dict(tblock=cfg.tblock, rows_per_wave=cfg.rows_per_wave, small_grid_lds=cfg.small_grid,
+                  tiled={"auto": -1, "on": 1, "off": 0}[cfg.tiled])
+        kw.update(getattr(self, "engine_kw", {}))
         return n.Engine(
             cfg.nx, cfg.ny, gridx=self.gridx, gridy=self.gridy, periodic_x=self.model.periodic_x,
             periodic_y=self.model.periodic_y, boundary=self.model.boundary_id(), precision=self.model.precision_id(),
-            init=self.model.init_id(), cx=self.model.cx, cy=self.model.cy, tblock=cfg.tblock,
-            rows_per_wave=cfg.rows_per_wave, convergence=cfg.convergence, interval=cfg.interval,
-            sensitivity=cfg.sensitivity, device=self.device, ranks=ranks, transport=transport,
-            overlap=cfg.overlap, small_grid_lds=cfg.small_grid, naive=cfg.naive)
+            init=self.model.init_id(), cx=self.model.cx, cy=self.model.cy, convergence=cfg.convergence,
+            interval=cfg.interval, sensitivity=cfg.sensitivity, device=self.device, ranks=ranks,
+            transport=transport, overlap=cfg.overlap, naive=cfg.naive, **kw)
 
     # ---- data access -------------------------------------------------------------------
     def tiles(self):

@@ -41,7 +41,7 @@ def test_poison_canary_cpu(native, boundary, gx, gy):
 def test_poison_canary_gpu(native, gpu, boundary, gx, gy, K):
     nx, ny, steps = 301, 517, 37  # ny % 4 != 0: partial-lane stores at the east edge
     eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=boundary, tblock=K, device=gpu, poison=True,
-                        small_grid_lds=False)
+                        small_grid_lds=False, tiled=0)
     eng.run(steps)
     assert np.array_equal(gather(eng, nx, ny), native.oracle_run(nx, ny, steps, boundary=boundary)["grid"])
 

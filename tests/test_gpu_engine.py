@@ -22,7 +22,7 @@ def oracle(n, nx, ny, steps, boundary=0, precision=0, init=0, per=(False, False)
 @pytest.mark.parametrize("boundary", [0, 1])
 def test_stream_single_tile_bitexact(native, gpu, nx, ny, boundary):
     steps = 23
-    eng = native.Engine(nx, ny, boundary=boundary, tblock=8, device=gpu, small_grid_lds=False)
+    eng = native.Engine(nx, ny, boundary=boundary, tblock=8, device=gpu, small_grid_lds=False, tiled=0)
     st = eng.run(steps)
     assert st["path"] == "stream" and st["steps_done"] == steps
     ref = oracle(native, nx, ny, steps, boundary)["grid"]
@@ -34,7 +34,7 @@ def test_stream_single_tile_bitexact(native, gpu, nx, ny, boundary):
 def test_every_compiled_K(native, gpu, K):
     nx, ny, steps = 203, 611, 2 * K + 3
     for boundary in (0, 1):
-        eng = native.Engine(nx, ny, boundary=boundary, tblock=K, device=gpu, small_grid_lds=False,
+        eng = native.Engine(nx, ny, boundary=boundary, tblock=K, device=gpu, small_grid_lds=False, tiled=0,
                             rows_per_wave=max(16, 4 * K))
         assert eng.halo_depth() == K
         eng.run(steps)
@@ -45,7 +45,7 @@ def test_every_compiled_K(native, gpu, K):
 @pytest.mark.parametrize("H", [1, 5, 16, 64, 300])
 def test_rows_per_wave_variants(native, gpu, H):
     nx, ny, steps = 150, 300, 17
-    eng = native.Engine(nx, ny, tblock=8, rows_per_wave=H, device=gpu, small_grid_lds=False)
+    eng = native.Engine(nx, ny, tblock=8, rows_per_wave=H, device=gpu, small_grid_lds=False, tiled=0)
     eng.run(steps)
     assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps)["grid"])
 
@@ -53,7 +53,7 @@ def test_rows_per_wave_variants(native, gpu, H):
 def test_int32_init_and_float_coeff(native, gpu):
     nx, ny, steps = 640, 512, 9
     cx = native.CX_FLOAT
-    eng = native.Engine(nx, ny, init=native.INIT_INT32, cx=cx, cy=cx, device=gpu, small_grid_lds=False)
+    eng = native.Engine(nx, ny, init=native.INIT_INT32, cx=cx, cy=cx, device=gpu, small_grid_lds=False, tiled=0)
     eng.run(steps)
     ref = oracle(native, nx, ny, steps, init=1, cx=cx, cy=cx)["grid"]
     assert np.array_equal(eng.download(0), ref)
@@ -61,7 +61,7 @@ def test_int32_init_and_float_coeff(native, gpu):
 
 def test_fp32_matches_cpu_fp32_and_torch(native, gpu):
     nx, ny, steps = 211, 333, 30
-    g = native.Engine(nx, ny, precision=native.FP32, device=gpu, small_grid_lds=False)
+    g = native.Engine(nx, ny, precision=native.FP32, device=gpu, small_grid_lds=False, tiled=0)
     g.run(steps)
     c = native.Engine(nx, ny, precision=native.FP32, device=-1)
     c.run(steps)
@@ -83,7 +83,7 @@ def test_fp32_matches_cpu_fp32_and_torch(native, gpu):
 def test_lds_small_grid_solver(native, gpu, nx, ny):
     steps = 1000
     for boundary in (0, 1):
-        eng = native.Engine(nx, ny, boundary=boundary, device=gpu)
+        eng = native.Engine(nx, ny, boundary=boundary, device=gpu, tiled=0)
         st = eng.run(steps)
         assert st["path"] == "lds"
         assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, boundary)["grid"])
@@ -215,3 +215,50 @@ def test_rccl_self_exchange_row_periodic(native, gpu, pipeline, contig, comm_cus
     eng.init_rccl(native.Engine.rccl_unique_id(), 1, 0)
     eng.run(steps)
     assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, boundary, per=(True, False))["grid"])
+
+
+# ---- LDS-tiled temporally-blocked path (tile_kernel.hip) --------------------------------
+TILE_SIZES = [(1, 1), (3, 2), (80, 64), (97, 131), (160, 128), (257, 509), (320, 256)]
+
+
+@pytest.mark.parametrize("nx,ny", TILE_SIZES)
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("width,K", [(64, 8), (128, 16), (64, 1), (128, 5)])
+def test_tiled_bitexact(native, gpu, nx, ny, boundary, width, K):
+    steps = 2 * K + 5  # full chunks and a partial one
+    eng = native.Engine(nx, ny, boundary=boundary, device=gpu, small_grid_lds=False, tiled=1, tile_width=width,
+                        tile_k=K, tile_rows=16, poison=True)
+    st = eng.run(steps)
+    assert st["path"] == "tiled" and st["steps_done"] == steps and eng.tile_config() == [16, width, K]
+    ref = oracle(native, nx, ny, steps, boundary)["grid"]
+    got = eng.download(0)
+    assert np.array_equal(got, ref), np.abs(got - ref).max()
+
+
+@pytest.mark.parametrize("per", [(True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_tiled_periodic(native, gpu, per, boundary):
+    nx, ny, steps = 45, 70, 29
+    eng = native.Engine(nx, ny, boundary=boundary, periodic_x=per[0], periodic_y=per[1], device=gpu, tiled=1,
+                        tile_k=6, tile_rows=8)
+    assert eng.run(steps)["path"] == "tiled"
+    assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, boundary, per=per)["grid"])
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_tiled_convergence_and_fp32(native, gpu, precision):
+    nx, ny = 120, 200
+    kw = dict(convergence=True, interval=7, sensitivity=5e3)
+    ref = oracle(native, nx, ny, 3000, 0, precision=precision, **kw)
+    eng = native.Engine(nx, ny, precision=precision, device=gpu, tiled=1, tile_k=8, small_grid_lds=False, **kw)
+    st = eng.run(3000)
+    assert st["path"] == "tiled"
+    assert st["steps_done"] == ref["steps_done"] and st["converged"] == ref["converged"]
+    assert np.array_equal(eng.download(0), ref["grid"])
+
+
+def test_tiled_auto_selection(native, gpu):
+    assert native.Engine(640, 512, device=gpu).tiled()
+    assert not native.Engine(4096, 4096, device=gpu).tiled()
+    assert not native.Engine(640, 512, gridx=2, device=gpu).tiled()  # several tiles
+    assert not native.Engine(640, 512, device=gpu, tiled=0).tiled()

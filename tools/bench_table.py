@@ -3,8 +3,8 @@ on one MI355X and print a markdown table next to the published times.
 
     python tools/bench_table.py [--steps 1000] [--precision ref] [--convergence]
 
-Each configuration runs through the same engine as the CLI (automatic path: whole-grid LDS
-solver for small grids, streaming kernel otherwise), W=200 untimed warm-up steps after a
+Each configuration runs through the same engine as the CLI (automatic path: LDS-tiled kernel
+for small and medium grids, streaming kernel otherwise; ``--tune`` times the candidates first), W=200 untimed warm-up steps after a
 0.2 s pre-warm, then the timed run (min of 3).
 """
 import argparse
@@ -45,11 +45,10 @@ def main():
 
     for (nx, ny) in SIZES + EXTRA:
         cfg = Config(nx=nx, ny=ny, precision=a.precision, boundary=a.boundary)
-        tb, H, lds = 8, 0, True
+        kw = {}
         if a.tune and nx * ny <= (1 << 22):
-            r = autotune(cfg, cfg.model(), 0)
-            tb, H, lds = r["tblock"], r["rows_per_wave"], r["small_grid"]
-        e = n.Engine(nx, ny, precision=prec, boundary=bnd, device=0, tblock=tb, rows_per_wave=H, small_grid_lds=lds)
+            kw = autotune(cfg, cfg.model(), 0)["engine_kw"]
+        e = n.Engine(nx, ny, precision=prec, boundary=bnd, device=0, **kw)
         t_end = time.perf_counter() + 0.2
         while time.perf_counter() < t_end:
             e.run(64)
@@ -65,7 +64,7 @@ def main():
             best = dt if best is None else min(best, dt)
             path = st["path"]
         cups = nx * ny * a.steps / best
-        rows.append(dict(grid=[nx, ny], steps=a.steps, seconds=best, cups=cups, path=path, tblock=tb, rows_per_wave=H,
+        rows.append(dict(grid=[nx, ny], steps=a.steps, seconds=best, cups=cups, path=path, engine_kw=kw,
                          cuda_ref_s=CUDA_1000.get((nx, ny)), mpi_best_s=MPI_BEST.get((nx, ny), (None, ""))[0],
                          mpi_best_cfg=MPI_BEST.get((nx, ny), (None, ""))[1], mpi_serial_s=MPI_SERIAL.get((nx, ny))))
     print(f"| grid | MI355X s ({a.steps} steps, {a.precision}) | cell-updates/s | path | ref CUDA s | ×CUDA | "

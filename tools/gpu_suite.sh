@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU session: the GPU test-suite, smoke(), the headline bench, and the multi-rank proxy
-# (row-periodic RCCL self-exchange on one GPU: the per-rank shape of the N>1 bench).
+# One GPU session: the GPU test-suite, smoke(), the headline bench, the multi-rank proxy
+# (row-periodic RCCL self-exchange on one GPU: the per-rank shape of the N>1 bench) and,
+# with TABLE=1, the reference-size tables.
 set -o pipefail
 mkdir -p gpurun_out
 export HEAT2D_NO_BUILD=1
@@ -12,3 +13,8 @@ cat gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/bench_ref.json 2> gpurun_out/bench_ref.err || exit $?
 cat gpurun_out/bench_ref.json
 timeout -k 10 120 python tools/overlap_trace.py one 2>&1 | grep us/step | tee gpurun_out/proxy.txt || exit $?
+if [ "${TABLE:-0}" = "1" ]; then
+  timeout -k 10 600 python tools/bench_table.py --json gpurun_out/table_ref.json > gpurun_out/table_ref.md 2>&1 || exit $?
+  timeout -k 10 600 python tools/bench_table.py --precision fp32 --json gpurun_out/table_fp32.json > gpurun_out/table_fp32.md 2>&1 || exit $?
+  grep -v amdgpu.ids gpurun_out/table_ref.md
+fi

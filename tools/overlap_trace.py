@@ -20,11 +20,11 @@ N = int(os.environ.get("OT_N", "4096"))
 
 def make(mode="rccl", **kw):
     if mode == "none":
-        return n.Engine(N, N, device=0, small_grid_lds=False, **kw)
+        return n.Engine(N, N, device=0, small_grid_lds=False, tiled=0, **kw)
     if mode == "local":
-        return n.Engine(N, N, periodic_x=True, boundary=1, device=0, small_grid_lds=False, **kw)
+        return n.Engine(N, N, periodic_x=True, boundary=1, device=0, small_grid_lds=False, tiled=0, **kw)
     e = n.Engine(N, N, periodic_x=True, boundary=1, device=0, ranks=[0], transport=n.TRANSPORT_RCCL,
-                 small_grid_lds=False, **kw)
+                 small_grid_lds=False, tiled=0, **kw)
     e.init_rccl(n.Engine.rccl_unique_id(), 1, 0)
     return e
 

@@ -17,7 +17,7 @@ ap.add_argument("--boundary", type=int, default=0)
 ap.add_argument("--periodic", action="store_true")
 a = ap.parse_args()
 n = heat2d_amd.native()
-e = n.Engine(a.n, a.n, precision=a.prec, tblock=a.K, rows_per_wave=a.H, device=0, small_grid_lds=False,
+e = n.Engine(a.n, a.n, precision=a.prec, tblock=a.K, rows_per_wave=a.H, device=0, small_grid_lds=False, tiled=0,
              boundary=a.boundary, edge_weight=a.ew, periodic_x=a.periodic, periodic_y=a.periodic)
 st = e.run(a.steps)
 e.synchronize()

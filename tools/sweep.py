@@ -33,7 +33,7 @@ def main():
                                    [int(h) for h in a.H.split(",")], [float(o) for o in a.ew.split(",")]))
     engines = {}
     for p, K, H, ew in cases:
-        e = n.Engine(a.n, ny, precision=p, tblock=K, rows_per_wave=H, device=0, small_grid_lds=False,
+        e = n.Engine(a.n, ny, precision=p, tblock=K, rows_per_wave=H, device=0, small_grid_lds=False, tiled=0,
                      edge_weight=ew, boundary=a.boundary, periodic_x=a.periodic, periodic_y=a.periodic)
         e.run(K * 4)
         engines[(p, K, H, ew)] = e
