@@ -14,7 +14,17 @@ from __future__ import annotations
 import importlib
 import os
 
-import torch  # noqa: F401  (must precede the native module, see above)
+# Hardware queues per process: the engine runs the compute stream and the comm stream (halo
+# exchange gate, RCCL, completion counter) concurrently, and HIP maps streams onto at most
+# GPU_MAX_HW_QUEUES in-order hardware queues.  With 4, streams created by other engines /
+# libraries shift the round-robin map until the two share one queue, which serialises the
+# exchange behind the stencil (measured: 9.5 -> 15 us/step on the multi-rank proxy,
+# tools/gpu_probe_queues.sh).  8 gives every stream its own queue.  Read once at HIP init,
+# so it is set here, before torch (or anything) touches the GPU.
+if os.environ.get("HEAT2D_KEEP_HW_QUEUES") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+import torch  # noqa: E402,F401  (must precede the native module, see above)
 
 _mod = None
 

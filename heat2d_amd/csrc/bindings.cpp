@@ -260,7 +260,7 @@ PYBIND11_MODULE(_heat2d, m) {
                        int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
                        bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s, bool trace, bool poison,
                        int comm_cus, int contiguous_halo, int comm_cu_layout, int reserve_waves,
-                       bool device_fence_events, int comm_boundary, int signal_exchange, int device_halo_wait, int tiled, int tile_rows, int tile_width, int tile_k) {
+                       bool device_fence_events, int comm_boundary, int signal_exchange, int device_halo_wait, int tiled, int tile_rows, int tile_width, int tile_k, int comm_priority, int signal_plan) {
              EngineOptions o;
              o.nx = nx;
              o.ny = ny;
@@ -303,6 +303,8 @@ PYBIND11_MODULE(_heat2d, m) {
              o.tile_rows = tile_rows;
              o.tile_width = tile_width;
              o.tile_k = tile_k;
+             o.comm_priority = comm_priority;
+             o.signal_plan = signal_plan;
              return new Engine(o);
            }),
            py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
@@ -316,7 +318,7 @@ PYBIND11_MODULE(_heat2d, m) {
            py::arg("watchdog_s") = 900.0, py::arg("trace") = false, py::arg("poison") = false,
            py::arg("comm_cus") = -1, py::arg("contiguous_halo") = -1, py::arg("comm_cu_layout") = 0, py::arg("reserve_waves") = -1,
            py::arg("device_fence_events") = false, py::arg("comm_boundary") = -1, py::arg("signal_exchange") = -1, py::arg("device_halo_wait") = -1,
-           py::arg("tiled") = -1, py::arg("tile_rows") = 0, py::arg("tile_width") = 0, py::arg("tile_k") = 0)
+           py::arg("tiled") = -1, py::arg("tile_rows") = 0, py::arg("tile_width") = 0, py::arg("tile_k") = 0, py::arg("comm_priority") = -1, py::arg("signal_plan") = -1)
       .def("num_tiles", &Engine::num_tiles)
       .def("tile_rank", &Engine::tile_rank)
       .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })

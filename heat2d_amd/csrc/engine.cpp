@@ -136,7 +136,15 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       H2D_HIP_CHECK(hipExtStreamCreateWithCUMask(&comm_, (uint32_t)mx.size(), mx.data()));
     } else {
       H2D_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
-      H2D_HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+      // Optionally a high-priority comm stream (its waves win dispatch ties against the
+      // stencil's).  Separate hardware queues for compute and comm come from
+      // GPU_MAX_HW_QUEUES >= 8 (heat2d_amd/_native.py), not from the priority.
+      int least = 0, greatest = 0;
+      if (o.comm_priority > 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least) {
+        H2D_HIP_CHECK(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, greatest));
+      } else {
+        H2D_HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+      }
     }
     // Pipeline events only order work on this device (RCCL fences its own cross-device
     // traffic), so they can skip the system-scope fence.
@@ -375,6 +383,56 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                    opt_.edge_weight, cap_in, peer, opt_.boundary_rows);
   }
+  // Signalled pipeline with only north/south peers (1-D row strips): no short boundary units.
+  // Every strip is cut into capacity-fitted units as if the tile had no peers; the top unit
+  // of a strip with a north peer and the bottom unit (streamed bottom-up) of a strip with a
+  // south peer become the signalling units: they wait for the halo, signal after their
+  // first K rows (the rows the exchange sends) and carry on with the rest of their rows.
+  // So the exchange starts early and no wave idles (the short-unit plan left nb waves idle
+  // for most of the launch and shrank the interior).
+  L.sig_rows = 0;
+  const bool ns_only = !peer[kW] && !peer[kE] && !peer[kNW] && !peer[kNE] && !peer[kSW] && !peer[kSE];
+  if (sig_mode_ > 0 && opt_.overlap && has_exchange_ && ns_only && (peer[kN] || peer[kS]) && opt_.signal_plan != 0) {
+    const int64_t reserve_sig = opt_.reserve_waves >= 0 ? opt_.reserve_waves : 16;
+    UnitPlan Q = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
+                            opt_.edge_weight, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, opt_.boundary_rows);
+    std::map<int, std::pair<int, int>> ends;  // strip -> (top unit, bottom unit) indices
+    for (int i = 0; i < (int)Q.interior.size(); ++i) {
+      const Unit& u = Q.interior[i];
+      auto e = ends.emplace(u.strip, std::make_pair(i, i)).first;
+      if (u.x0 < Q.interior[e->second.first].x0) e->second.first = i;
+      if (u.x0 > Q.interior[e->second.second].x0) e->second.second = i;
+    }
+    bool ok = true;
+    std::vector<int> role(Q.interior.size(), 0);  // 1 top, 2 bottom (reverse), 3 both (signal at end)
+    for (auto& kv : ends) {
+      const int ti = kv.second.first, bi = kv.second.second;
+      if (ti == bi) {
+        if (peer[kN] || peer[kS]) role[ti] = 3;
+        continue;
+      }
+      if (peer[kN]) role[ti] = 1;
+      if (peer[kS]) role[bi] = 2;
+      // the neighbouring units' K-cones must not reach the ghost rows
+      if ((peer[kN] && Q.interior[ti].h < K) || (peer[kS] && Q.interior[bi].h < K)) ok = false;
+    }
+    if (ok) {
+      std::vector<Unit> sg, rest;
+      for (int i = 0; i < (int)Q.interior.size(); ++i) {
+        Unit u = Q.interior[i];
+        if (role[i] == 0) {
+          rest.push_back(u);
+          continue;
+        }
+        if (role[i] == 2) u.flags |= kUnitReverse;
+        if (role[i] == 3) u.flags |= kUnitSigEnd;
+        sg.push_back(u);
+      }
+      P.interior = rest;
+      P.boundary = sg;
+      L.sig_rows = K;
+    }
+  }
   std::vector<Unit>& in = P.interior;
   std::vector<Unit>& bd = P.boundary;
   std::vector<Unit> all = in;
@@ -449,6 +507,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     a.prot = L.n_interior;
     a.signal = sig_counter_;
     a.nsignal = L.n_boundary;
+    a.sig_rows = L.sig_rows;
     sig_target_ += (unsigned long long)L.n_boundary;
     if (dev_wait_) {
       a.halo_ready = halo_counter_;

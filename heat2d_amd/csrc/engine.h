@@ -65,6 +65,11 @@ struct EngineOptions {
   // poll a counter the comm stream sets after the exchange), so the compute stream never
   // waits on the comm stream.  -1 auto (on), 0: the chunk launch waits on an event instead.
   int device_halo_wait = -1;
+  // comm stream priority: 1 high, 0 / -1 normal (default; high was not faster on one GPU)
+  int comm_priority = -1;
+  // signalled pipeline unit plan for 1-D row strips: -1/1 full-size signalling units (mid-unit
+  // signal, bottom units streamed bottom-up), 0 short boundary units (signal at their end)
+  int signal_plan = -1;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
   bool poison = false;        // debug canary: NaN in every cell no valid update may read
@@ -183,6 +188,7 @@ class Engine {
     Unit* d_interior = nullptr;
     Unit* d_boundary = nullptr;
     Unit* d_bfirst = nullptr;  // boundary units, then interior units (signalled pipeline)
+    int sig_rows = 0;          // > 0: boundary units are full-size and signal after this many rows
     int n_all = 0, n_interior = 0, n_boundary = 0;
   };
 

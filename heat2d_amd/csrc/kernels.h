@@ -25,13 +25,16 @@ namespace h2d {
 // Work unit of the streaming kernel: one wave = one 256-column strip × rows [x0, x0+h).
 // flags: kEdgeCols — a column of the strip's window is a global edge / outside the grid;
 //        kEdgeRows — a row of the unit's K-cone is.  Computed on the host (unit_edge_flags).
+//        kUnitReverse — the wave streams its rows bottom-up (a bottom halo unit of the
+//        signalled pipeline: its halo-dependent rows come first);
+//        kUnitSigEnd — a signalling unit that signals at its end, not after sig_rows rows.
 struct Unit {
   int strip;
   int x0;
   int h;
   int flags;
 };
-constexpr int kEdgeCols = 1, kEdgeRows = 2;
+constexpr int kEdgeCols = 1, kEdgeRows = 2, kUnitReverse = 4, kUnitSigEnd = 8;
 
 int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t y0, bool fixed, bool per_x, bool per_y);
 // Cut a tile into work units for depth K: ~H rows per unit, edge units shortened by
@@ -73,6 +76,9 @@ struct StreamArgs {
   // 1 to *signal when done, so the comm stream can start the exchange mid-kernel.
   int nsignal = 0;
   unsigned long long* signal = nullptr;
+  // > 0: a signalling unit signals as soon as its first sig_rows output rows (in streaming
+  // order) are stored, then carries on with the rest of its rows (kUnitSigEnd: at its end)
+  int sig_rows = 0;
   // Device-side halo wait: units [0, nsignal) first poll *halo_ready until it reaches
   // halo_need (the exchange that fills their ghost rows has landed); after halo_polls polls
   // they give up and set bit 2 of *timed_out.

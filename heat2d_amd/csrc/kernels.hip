@@ -74,6 +74,7 @@ __global__ __launch_bounds__(256) void reduce_sum_kernel(const double* __restric
 __global__ __launch_bounds__(64) void wait_counter_kernel(const unsigned long long* counter, unsigned long long target,
                                                           unsigned int* timed_out, long long max_polls) {
   if (threadIdx.x != 0) return;
+  if (__hip_atomic_load(timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;  // fail fast
   for (long long i = 0; i < max_polls; ++i) {
     if (__hip_atomic_load(counter, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= target) return;
     __builtin_amdgcn_s_sleep(4);

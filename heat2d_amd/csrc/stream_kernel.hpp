@@ -79,6 +79,7 @@ __device__ __forceinline__ float4 row_update(const float4& P, const float4& C, c
 
 struct LaneCtx {
   int64_t gxb;     // global row of stream input index 0
+  int64_t dir;     // +1: rows stream top-down, -1: bottom-up (kUnitReverse)
   int64_t NX;
   bool m0, m1, m2, m3;  // per-column mask: fixed -> hold (global edge), ghost-zero -> zero (outside)
   float* sout;     // real output pointer (lanes in the output range), or a dummy slot
@@ -144,7 +145,7 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
     const float4 prv = S[t - 1][P];
     const float4 mid = S[t - 1][1 - P];
     float4 o = row_update<F32>(prv, mid, cur, k);
-    if constexpr (EDGE != 0) o = apply_edge<EDGE, FIXED>(o, mid, c.gxb + ir - t, c);
+    if constexpr (EDGE != 0) o = apply_edge<EDGE, FIXED>(o, mid, c.gxb + c.dir * (ir - t), c);
     S[t - 1][P] = cur;
     if (t == K) {
       const int64_t orow = ir - 2 * K;
@@ -171,9 +172,19 @@ __device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4* __rest
   }
 }
 
+// Mid-unit signal of the signalled halo pipeline: this wave's halo rows are stored — release
+// them at system scope and count the unit.
+__device__ __forceinline__ void unit_signal(unsigned long long* sig, int lane) {
+  __threadfence_system();
+  if (lane == 0) __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// sig_at > 0: signal (once) before processing stream row sig_at (a multiple of 4 past 2K),
+// i.e. once every output row < sig_at - 2K is stored.
 template <int K, bool F32, int EDGE, bool FIXED, bool RESID>
 __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, int64_t pitch4, int n, const LaneCtx& c,
-                                         const Coef& k, double& racc) {
+                                         const Coef& k, double& racc, int sig_at, unsigned long long* sig,
+                                         int lane) {
   float4 S[K][2];
 #pragma unroll
   for (int t = 0; t < K; ++t) {
@@ -194,6 +205,7 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, int64_
     process_row<K, F32, EDGE, FIXED, RESID, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
   for (; ir0 + 4 <= n; ir0 += 4) {
+    if (ir0 == sig_at) unit_signal(sig, lane);
     H2D_STEADY(0)
     H2D_STEADY(1)
     H2D_STEADY(2)
@@ -204,6 +216,9 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, int64_
   if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, 0, K>(S, pf[0], ir0, c, k, racc);
   if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
   if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
+  // the loop visits every sig_at candidate below its exit value: a signal point at or past the
+  // exit has not fired yet (unit shorter than its signal rows, or kUnitSigEnd)
+  if (sig_at >= ir0) unit_signal(sig, lane);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -214,9 +229,9 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 template <int K, bool F32, bool RESID, int EDGE>
 __device__ __forceinline__ void run_edge(const float4* rowp, int64_t pitch4, int n, const LaneCtx& c, const Coef& k,
-                                         double& racc, bool fixed) {
-  if (fixed) run_unit<K, F32, EDGE, true, RESID>(rowp, pitch4, n, c, k, racc);
-  else run_unit<K, F32, EDGE, false, RESID>(rowp, pitch4, n, c, k, racc);
+                                         double& racc, bool fixed, int sig_at, unsigned long long* sig, int lane) {
+  if (fixed) run_unit<K, F32, EDGE, true, RESID>(rowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+  else run_unit<K, F32, EDGE, false, RESID>(rowp, pitch4, n, c, k, racc, sig_at, sig, lane);
 }
 
 template <int K, bool F32, bool RESID>
@@ -227,7 +242,8 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const int lane = (int)(threadIdx.x & 63);
   if (a.halo_ready != nullptr && w < a.nsignal) {
     // halo-dependent unit: wait until the exchange that fills its ghost rows has landed
-    if (lane == 0) {
+    // (a gate that already timed out in this engine stops every later wait: fail fast)
+    if (lane == 0 && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
       long long i = 0;
       while (__hip_atomic_load(a.halo_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.halo_need) {
         if (++i > a.halo_polls) {
@@ -245,8 +261,13 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const int h = u.h;
   const int64_t cb = y0 - a.R + 4 * lane;
 
+  // kUnitReverse: stream the unit's rows bottom-up (negative pitches)
+  const bool rev = (u.flags & kUnitReverse) != 0;
+  const int64_t xin = rev ? x0 + h - 1 + K : x0 - K;  // first stream row (tile row)
+  const int64_t xout = rev ? x0 + h - 1 : x0;         // first output row
   LaneCtx c;
-  c.gxb = a.gx0 + x0 - K;
+  c.gxb = a.gx0 + xin;
+  c.dir = rev ? -1 : 1;
   c.NX = a.NX;
   const int64_t gc = a.gy0 + cb;
   const bool fixed = a.fixed != 0;
@@ -260,36 +281,35 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   // Lanes in the output range store a full float4 (columns past ycell land in the ghost /
   // pad columns inside the pitch and hold valid cone values there); others hit a dummy slot.
   const bool in_out = (cb >= y0) && (cb + 4 <= y0 + a.wout) && (cb < a.ycell);
-  float* out = a.dst + (a.G + x0) * a.pitch + a.PL + cb;
+  float* out = a.dst + (a.G + xout) * a.pitch + a.PL + cb;
   c.sout = in_out ? out : a.dummy + 4 * lane;
-  c.spitch = in_out ? a.pitch : 0;
+  c.spitch = in_out ? (rev ? -a.pitch : a.pitch) : 0;
   c.st0 = in_out;
   c.st1 = in_out && cb + 1 < a.ycell;
   c.st2 = in_out && cb + 2 < a.ycell;
   c.st3 = in_out && cb + 3 < a.ycell;
 
-  const float4* rowp = reinterpret_cast<const float4*>(a.src + (a.G + x0 - K) * a.pitch + a.PL + cb);
-  const int64_t pitch4 = a.pitch >> 2;
+  const float4* rowp = reinterpret_cast<const float4*>(a.src + (a.G + xin) * a.pitch + a.PL + cb);
+  const int64_t pitch4 = rev ? -(a.pitch >> 2) : (a.pitch >> 2);
   const int n = h + 2 * K;
   Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
   double racc = 0.0;
+  // signalling units: mid-unit signal point (or the end); others never signal
+  const bool sig_unit = a.signal != nullptr && w < a.nsignal;
+  const int sig_at = !sig_unit ? -1
+                     : ((u.flags & kUnitSigEnd) != 0 || a.sig_rows <= 0) ? (1 << 30)
+                                                                          : 2 * K + ((a.sig_rows + 3) & ~3);
   switch (u.flags & 3) {
-    case 0: run_unit<K, F32, 0, false, RESID>(rowp, pitch4, n, c, k, racc); break;
-    case 1: run_edge<K, F32, RESID, 1>(rowp, pitch4, n, c, k, racc, fixed); break;
-    case 2: run_edge<K, F32, RESID, 2>(rowp, pitch4, n, c, k, racc, fixed); break;
-    default: run_edge<K, F32, RESID, 3>(rowp, pitch4, n, c, k, racc, fixed); break;
+    case 0: run_unit<K, F32, 0, false, RESID>(rowp, pitch4, n, c, k, racc, sig_at, a.signal, lane); break;
+    case 1: run_edge<K, F32, RESID, 1>(rowp, pitch4, n, c, k, racc, fixed, sig_at, a.signal, lane); break;
+    case 2: run_edge<K, F32, RESID, 2>(rowp, pitch4, n, c, k, racc, fixed, sig_at, a.signal, lane); break;
+    default: run_edge<K, F32, RESID, 3>(rowp, pitch4, n, c, k, racc, fixed, sig_at, a.signal, lane); break;
   }
   if constexpr (RESID) {
     racc = wave_sum(racc);
     int slot = w + a.prot;
     if (slot >= a.nunits) slot -= a.nunits;
     if (lane == 0) a.partials[slot] = racc;
-  }
-  if (a.signal != nullptr && w < a.nsignal) {
-    // halo rows of this unit are final: make them visible device- and system-wide (the
-    // exchange may read them from another queue or over xGMI), then count the unit
-    __threadfence_system();
-    if (lane == 0) __hip_atomic_fetch_add(a.signal, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

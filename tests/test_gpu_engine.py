@@ -167,15 +167,18 @@ def test_rccl_convergence_allreduce(native, gpu):
 # stream (two streams), 2 concurrent with a boundary stream of its own (three streams),
 # 3 signalled (one launch per chunk, exchange gated mid-kernel by hipStreamWaitValue64),
 # 4 signalled with a polling-kernel gate (the default), 5 the same with the chunk launch waiting on
-# a halo event instead of the in-kernel halo wait
+# a halo event instead of the in-kernel halo wait, 6 signalled with short boundary units instead
+# of full-size mid-unit-signalling ones
 PIPELINES = {0: dict(concurrent=0, signal_exchange=0), 1: dict(concurrent=1, signal_exchange=0),
              2: dict(concurrent=1, comm_boundary=0, signal_exchange=0), 3: dict(signal_exchange=1),
-             4: dict(signal_exchange=2), 5: dict(signal_exchange=2, device_halo_wait=0)}
-PIPELINE_NAMES = {0: "boundary-first", 1: "concurrent", 2: "concurrent3", 3: "signal", 4: "signal", 5: "signal"}
+             4: dict(signal_exchange=2), 5: dict(signal_exchange=2, device_halo_wait=0),
+             6: dict(signal_exchange=2, signal_plan=0)}
+PIPELINE_NAMES = {0: "boundary-first", 1: "concurrent", 2: "concurrent3", 3: "signal", 4: "signal", 5: "signal",
+                  6: "signal"}
 
 
 @pytest.mark.parametrize("gx,gy", [(2, 1), (4, 1), (2, 2), (1, 3)])
-@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5, 6])
 def test_overlap_pipelines(native, gpu, gx, gy, pipeline):
     """Boundary-first and concurrent pipelines, with convergence."""
     nx, ny, steps = 257, 509, 45
@@ -201,7 +204,7 @@ def test_pipeline_auto(native, gpu):
     assert native.Engine(2048, 2048, device=gpu).pipeline() == "none"
 
 
-@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("contig,comm_cus", [(0, 0), (1, 0), (1, 8), (0, 4)])
 @pytest.mark.parametrize("boundary", [0, 1])
 def test_rccl_self_exchange_row_periodic(native, gpu, pipeline, contig, comm_cus, boundary):

@@ -46,19 +46,16 @@ if sys.argv[1:2] == ["one"]:
     sys.exit(0)
 
 cases = {"none (no exchange)": make("none")}
-for cc in (1, 0):
-    for contig in (0, 1):
-        for cus in (0, 4, 8, 16):
-            for br in (8, 16):
-                if cc == 0 and (br != 16 or cus not in (0, 8)):
-                    continue
-                cases[f"rccl cc={cc} contig={contig} comm_cus={cus:2d} brows={br:2d}"] = make(
-                    concurrent=cc, contiguous_halo=contig, comm_cus=cus, boundary_rows=br)
+for spec in (sys.argv[2:] if sys.argv[1:2] == ["matrix"] and len(sys.argv) > 2 else
+             ["signal_exchange=2", "signal_exchange=2 reserve_waves=0", "signal_exchange=2 reserve_waves=8",
+              "signal_exchange=0 concurrent=1", "signal_exchange=0 concurrent=0"]):
+    kw = {k: int(v) for k, v in (t.split("=") for t in spec.split())}
+    cases["rccl " + spec] = make("rccl", **kw)
 for e in cases.values():
-    e.run(400)
+    e.run(800)
 res = {k: [] for k in cases}
-for r in range(3):
+for r in range(5):  # interleaved repeats: clock drift hits every case alike
     for k, e in cases.items():
         res[k].append(timeit(e))
 for k, v in res.items():
-    print(f"{k:50s} {min(v):8.2f} us/step")
+    print(f"{k:50s} min {min(v):7.2f}  median {sorted(v)[len(v) // 2]:7.2f} us/step")
