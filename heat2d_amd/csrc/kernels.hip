@@ -76,7 +76,8 @@ __global__ __launch_bounds__(64) void wait_counter_kernel(const unsigned long lo
   if (threadIdx.x != 0) return;
   if (__hip_atomic_load(timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;  // fail fast
   for (long long i = 0; i < max_polls; ++i) {
-    if (__hip_atomic_load(counter, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= target) return;
+    // relaxed: this wave reads no payload (the exchange kernel behind it acquires at its start)
+    if (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= target) return;
     __builtin_amdgcn_s_sleep(4);
   }
   __hip_atomic_fetch_or(timed_out, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
