@@ -484,6 +484,15 @@ PYBIND11_MODULE(_heat2d, m) {
         return out;
       },
       "work units (strip, x0, h, flags) of a single nx×ny tile");
+  m.def(
+      "strip_layout",
+      [](int64_t nx, int64_t ny, int K, bool fixed, bool per_y) {
+        const TileGeom g = make_tile_geom(nx, ny, 0, 0, nx, ny, K);
+        py::list out;
+        for (const Strip& s : strip_layout(g, K, fixed, per_y)) out.append(py::make_tuple(s.cb, s.lo, s.hi));
+        return out;
+      },
+      "column strips (cb, lo, hi) of a single nx×ny tile: lane-0 column, output columns [lo, hi)");
   m.def("lead_cols", &lead_cols);
   m.def("strip_out_cols", &strip_out_cols);
 }

@@ -68,7 +68,8 @@ TileGeom make_tile_geom(int64_t NX, int64_t NY, int64_t gx0, int64_t gy0, int64_
   const int64_t R = g.PL;
   // Strips of the widest kernel we may launch (smallest K=1 has the widest output strip,
   // largest K the most strips): size the pitch for the worst case over K in [1, G].
-  int64_t need = g.PL + ycell + G;  // owned + right ghost
+  // owned + right ghost; an edge-aligned last strip's window ends at round_up(ycell, 4)
+  int64_t need = g.PL + std::max(ycell + G, (ycell + 3) & ~int64_t(3));
   for (int64_t K = 1; K <= std::max<int64_t>(1, G); ++K) {
     const int64_t r = lead_cols((int)K);
     const int64_t wout = kWaveCols - 2 * r;

@@ -28,15 +28,27 @@ namespace h2d {
 //        kUnitReverse — the wave streams its rows bottom-up (a bottom halo unit of the
 //        signalled pipeline: its halo-dependent rows come first);
 //        kUnitSigEnd — a signalling unit that signals at its end, not after sig_rows rows.
+// cb: tile column of lane 0's first element (the wave's 256-column window is [cb, cb+256));
+// [olo, ohi): the strip's output columns.  Interior strips have cb = olo - R; a strip against
+// a FIXED global edge column is aligned to that edge and needs no outer cone (the held edge
+// column is valid at every level), so it outputs 256 - R columns (strip_layout).
 struct Unit {
   int strip;
   int x0;
   int h;
   int flags;
+  int cb, olo, ohi;
 };
 constexpr int kEdgeCols = 1, kEdgeRows = 2, kUnitReverse = 4, kUnitSigEnd = 8;
 
-int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t y0, bool fixed, bool per_x, bool per_y);
+int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t cb, bool fixed, bool per_x, bool per_y);
+// Column strips of a tile for depth K.  Interior strips output 256 - 2R columns; with fixed
+// edges a strip at a global edge column is edge-aligned and outputs 256 - R (4096 columns at
+// K=8: 248 + 15×240 + 248 = 17 strips instead of 18).
+struct Strip {
+  int64_t cb, lo, hi;
+};
+std::vector<Strip> strip_layout(const TileGeom& g, int K, bool fixed, bool per_y);
 // Cut a tile into work units for depth K: ~H rows per unit, edge units shortened by
 // `edge_weight` so that every wave finishes at about the same time (one wave round).
 // H > 0 fixes the rows of a plain unit; H == 0 sizes units to fill `capacity` resident waves.

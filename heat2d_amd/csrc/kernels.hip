@@ -235,10 +235,30 @@ int64_t stream_wave_capacity(int K, int precision, int device) {
   return (int64_t)bpc * cus * 4;
 }
 
-int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t y0, bool fixed, bool per_x, bool per_y) {
+std::vector<Strip> strip_layout(const TileGeom& g, int K, bool fixed, bool per_y) {
+  const int64_t R = lead_cols(K), wout = strip_out_cols(K);
+  const bool wide = fixed && !per_y && g.ycell >= kWaveCols;
+  const bool lo_edge = wide && g.gy0 == 0;
+  const bool hi_edge = wide && g.gy0 + g.ycell == g.NY;
+  std::vector<Strip> v;
+  int64_t a = 0, b = g.ycell, rcb = 0;
+  if (lo_edge) {
+    v.push_back(Strip{0, 0, kWaveCols - R});
+    a = kWaveCols - R;
+  }
+  if (hi_edge) {
+    rcb = ((g.ycell + 3) & ~int64_t(3)) - kWaveCols;  // window ends at the (4-aligned) edge
+    b = std::max(a, rcb + R);
+  }
+  for (int64_t p = a; p < b; p += wout) v.push_back(Strip{p - R, p, std::min(p + wout, b)});
+  if (hi_edge && b < g.ycell) v.push_back(Strip{rcb, b, g.ycell});
+  return v;
+}
+
+int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t cb, bool fixed, bool per_x, bool per_y) {
   int f = 0;
   if (!per_y) {
-    const int64_t lo = g.gy0 + y0 - lead_cols(K), hi = lo + kWaveCols - 1;  // the wave's column window
+    const int64_t lo = g.gy0 + cb, hi = lo + kWaveCols - 1;  // the wave's column window
     const bool sp = fixed ? ((lo <= 0 && 0 <= hi) || (lo <= g.NY - 1 && g.NY - 1 <= hi)) : (lo < 0 || hi >= g.NY);
     if (sp) f |= kEdgeCols;
   }
@@ -260,10 +280,10 @@ struct RowRange {
 // Cut every range into units of (nearly) equal cost, fitting `capacity` waves in one round.
 // A unit of h rows costs ~ (h + K) wave-row-steps (the 2K-row prologue primes K levels); an
 // edge unit costs w times more: target cost U -> h = U - K (plain) or U/w - K (edge).
-std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<RowRange>& ranges, int H, bool fixed,
-                              bool per_x, bool per_y, double edge_weight, int64_t capacity) {
+std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>& strips,
+                              const std::vector<RowRange>& ranges, int H, bool fixed, bool per_x, bool per_y,
+                              double edge_weight, int64_t capacity) {
   const double w = std::max(1.0, edge_weight);
-  const int64_t wout = strip_out_cols(K);
   auto rows_for = [&](double U, bool edge) { return std::max<int64_t>(1, (int64_t)(edge ? U / w - K : U - K)); };
   auto plan = [&](double U, std::vector<Unit>* out) -> int64_t {
     int64_t count = 0;
@@ -275,8 +295,10 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<RowRan
       if (out)
         for (int64_t i = 0; i < n; ++i) {
           const int64_t s0 = a + len * i / n, s1 = a + len * (i + 1) / n;
+          const Strip& S = strips[(size_t)strip];
           out->push_back(Unit{(int)strip, (int)s0, (int)(s1 - s0),
-                              unit_edge_flags(g, K, s0, s1 - s0, strip * wout, fixed, per_x, per_y)});
+                              unit_edge_flags(g, K, s0, s1 - s0, S.cb, fixed, per_x, per_y), (int)S.cb,
+                              (int)S.lo, (int)S.hi});
         }
     };
     for (const RowRange& r : ranges) {
@@ -324,18 +346,19 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<RowRan
 UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
                     int64_t capacity, const bool* peer, int hb) {
   UnitPlan P;
-  const int64_t wout = strip_out_cols(K);
-  const int64_t nstrips = (g.ycell + wout - 1) / wout;
+  const std::vector<Strip> strips = strip_layout(g, K, fixed, per_y);
+  const int64_t nstrips = (int64_t)strips.size();
   hb = std::max(hb, K);
   const bool has_peer = peer && std::any_of(peer, peer + kNumDirs, [](bool b) { return b; });
   const bool top_bd = has_peer && (peer[kN] || peer[kNW] || peer[kNE]);
   const bool bot_bd = has_peer && (peer[kS] || peer[kSW] || peer[kSE]);
   std::vector<RowRange> in_r, bd_r;
   for (int64_t s = 0; s < nstrips; ++s) {
-    const int64_t y0 = s * wout, y1 = std::min(g.ycell, y0 + wout);
-    const bool col_edge = unit_edge_flags(g, K, 0, 1, y0, fixed, true, per_y) & kEdgeCols;
-    const bool row_edge_top = unit_edge_flags(g, K, 0, 1, y0, fixed, per_x, true) & kEdgeRows;
-    const bool row_edge_bot = unit_edge_flags(g, K, g.xcell - 1, 1, y0, fixed, per_x, true) & kEdgeRows;
+    const Strip& S = strips[(size_t)s];
+    const int64_t y0 = S.lo, y1 = S.hi;
+    const bool col_edge = unit_edge_flags(g, K, 0, 1, S.cb, fixed, true, per_y) & kEdgeCols;
+    const bool row_edge_top = unit_edge_flags(g, K, 0, 1, S.cb, fixed, per_x, true) & kEdgeRows;
+    const bool row_edge_bot = unit_edge_flags(g, K, g.xcell - 1, 1, S.cb, fixed, per_x, true) & kEdgeRows;
     const bool lr_bd = has_peer && ((y0 - K < 0 && (peer[kW] || peer[kNW] || peer[kSW])) ||
                                     (y1 + K > g.ycell && (peer[kE] || peer[kNE] || peer[kSE])));
     if (lr_bd) {
@@ -356,9 +379,9 @@ UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, boo
       in_r.push_back(RowRange{s, top, bot, col_edge});
     }
   }
-  P.interior = size_ranges(g, K, in_r, H, fixed, per_x, per_y, edge_weight, capacity);
+  P.interior = size_ranges(g, K, strips, in_r, H, fixed, per_x, per_y, edge_weight, capacity);
   // Boundary units are short (hb rows): they run first, alone, and gate the halo exchange.
-  P.boundary = size_ranges(g, K, bd_r, hb, fixed, per_x, per_y, 1.0, capacity);
+  P.boundary = size_ranges(g, K, strips, bd_r, hb, fixed, per_x, per_y, 1.0, capacity);
   auto edge_first = [](const Unit& a, const Unit& b) { return (a.flags != 0) > (b.flags != 0); };
   std::stable_sort(P.interior.begin(), P.interior.end(), edge_first);
   return P;

@@ -34,11 +34,13 @@ namespace h2d {
 namespace {
 
 // lane i <- lane i-1 (DPP wave_shr:1), lane i <- lane i+1 (DPP wave_shl:1).
+// bound_ctrl=1 (lanes without a source read 0, the add identity) lets the compiler fold the
+// DPP move into the consuming v_add_f32 (one VALU op instead of two).
 __device__ __forceinline__ float from_left(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float from_right(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 struct Coef {
@@ -46,11 +48,10 @@ struct Coef {
   float cxf, cyf;
 };
 
-// Device cell update; identical values to update_ref / update_f32 (h2d_common.h).
+// Device cell update from the fp32 pair sums sn = s+n, ew = e+w; identical values to
+// update_ref / update_f32 (h2d_common.h).
 template <bool F32>
-__device__ __forceinline__ float cell(float c, float n, float s, float w, float e, const Coef& k) {
-  const float sn = s + n;
-  const float ew = e + w;
+__device__ __forceinline__ float cell(float c, float sn, float ew, const Coef& k) {
   if constexpr (F32) {
     const float r = __builtin_fmaf(k.cxf, __builtin_fmaf(-2.0f, c, sn), c);
     return __builtin_fmaf(k.cyf, __builtin_fmaf(-2.0f, c, ew), r);
@@ -64,16 +65,29 @@ __device__ __forceinline__ float cell(float c, float n, float s, float w, float 
   }
 }
 
+template <bool F32>
+__device__ __forceinline__ float cell(float c, float n, float s, float w, float e, const Coef& k) {
+  return cell<F32>(c, s + n, e + w, k);
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // One row of one time level: P = row i-1, C = row i, N = row i+1 of the previous level.
+// The eight fp32 pair sums take five VALU ops: three packed adds (v_pk_add_f32, two lanes of
+// fp32 per op, same IEEE rounding as v_add_f32) and two adds with the DPP neighbour fetch
+// folded in (v_add_f32_dpp).
 template <bool F32>
 __device__ __forceinline__ float4 row_update(const float4& P, const float4& C, const float4& N, const Coef& k) {
-  const float l = from_left(C.w);
-  const float r = from_right(C.x);
+  const f32x2 sn01 = f32x2{P.x, P.y} + f32x2{N.x, N.y};
+  const f32x2 sn23 = f32x2{P.z, P.w} + f32x2{N.z, N.w};
+  const f32x2 ew12 = f32x2{C.x, C.y} + f32x2{C.z, C.w};  // (C.x + C.z, C.y + C.w)
+  const float ew0 = from_left(C.w) + C.y;
+  const float ew3 = C.z + from_right(C.x);
   float4 o;
-  o.x = cell<F32>(C.x, P.x, N.x, l, C.y, k);
-  o.y = cell<F32>(C.y, P.y, N.y, C.x, C.z, k);
-  o.z = cell<F32>(C.z, P.z, N.z, C.y, C.w, k);
-  o.w = cell<F32>(C.w, P.w, N.w, C.z, r, k);
+  o.x = cell<F32>(C.x, sn01.x, ew0, k);
+  o.y = cell<F32>(C.y, sn01.y, ew12.x, k);
+  o.z = cell<F32>(C.z, sn23.x, ew12.y, k);
+  o.w = cell<F32>(C.w, sn23.y, ew3, k);
   return o;
 }
 
@@ -261,10 +275,9 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   const Unit u = a.units[w];
-  const int64_t y0 = (int64_t)u.strip * a.wout;
   const int64_t x0 = u.x0;
   const int h = u.h;
-  const int64_t cb = y0 - a.R + 4 * lane;
+  const int64_t cb = (int64_t)u.cb + 4 * lane;
 
   // kUnitReverse: stream the unit's rows bottom-up (negative pitches)
   const bool rev = (u.flags & kUnitReverse) != 0;
@@ -285,7 +298,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   c.m3 = colmask(gc + 3);
   // Lanes in the output range store a full float4 (columns past ycell land in the ghost /
   // pad columns inside the pitch and hold valid cone values there); others hit a dummy slot.
-  const bool in_out = (cb >= y0) && (cb + 4 <= y0 + a.wout) && (cb < a.ycell);
+  const bool in_out = (cb >= u.olo) && (cb < u.ohi);
   float* out = a.dst + (a.G + xout) * a.pitch + a.PL + cb;
   c.sout = in_out ? out : a.dummy + 4 * lane;
   c.spitch = in_out ? (rev ? -a.pitch : a.pitch) : 0;

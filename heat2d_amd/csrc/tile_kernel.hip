@@ -94,10 +94,14 @@ __global__ __launch_bounds__(256) void tile_lds_kernel(TileArgs a) {
       const float4 S = *reinterpret_cast<const float4*>(p + W);
       const float wv = p[-1], ev = p[4];
       float4 o;
-      o.x = cell<F32>(C.x, N.x, S.x, wv, C.y, k);
-      o.y = cell<F32>(C.y, N.y, S.y, C.x, C.z, k);
-      o.z = cell<F32>(C.z, N.z, S.z, C.y, C.w, k);
-      o.w = cell<F32>(C.w, N.w, S.w, C.z, ev, k);
+      // packed fp32 pair sums (fp32 add is commutative, so the values match s+n / e+w)
+      const f32x2 sn01 = f32x2{N.x, N.y} + f32x2{S.x, S.y};
+      const f32x2 sn23 = f32x2{N.z, N.w} + f32x2{S.z, S.w};
+      const f32x2 ew12 = f32x2{C.x, C.y} + f32x2{C.z, C.w};
+      o.x = cell<F32>(C.x, sn01.x, wv + C.y, k);
+      o.y = cell<F32>(C.y, sn01.y, ew12.x, k);
+      o.z = cell<F32>(C.z, sn23.x, ew12.y, k);
+      o.w = cell<F32>(C.w, sn23.y, C.z + ev, k);
       const int gr = x0 + r;
       bool rm = false;
       if (!a.per_x) rm = a.fixed ? (gr == 0 || gr == a.NX - 1) : (gr < 0 || gr >= a.NX);

@@ -130,8 +130,18 @@ def test_resume_equals_uninterrupted(native):
 def test_unit_planner_covers_rows_and_packs_rounds(native, n, cap):
     K = 8
     units = native.unit_plan(n, n, K, 0, True, False, False, 1.2, cap)
-    wout = native.strip_out_cols(K)
-    nstrips = (n + wout - 1) // wout
+    strips = native.strip_layout(n, n, K, True, False)
+    nstrips = len(strips)
+    # output columns tile [0, n) without overlap; windows stay inside the padded row
+    R, pos = native.lead_cols(K), 0
+    for cb, lo, hi in strips:
+        assert lo == pos and hi > lo and cb % 4 == 0
+        assert cb + R <= lo or cb == 0  # left cone inside the window (or edge-aligned)
+        assert hi <= cb + 256 - R or cb + 256 >= n  # right cone inside the window (or edge-aligned)
+        pos = hi
+    assert pos == n
+    if n == 4096:
+        assert nstrips == 17  # 248 + 15 x 240 + 248
     rows = {}
     for s, x0, h, flags in units:
         rows.setdefault(s, []).append((x0, h))

@@ -10,7 +10,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [(1, 1), (2, 3), (7, 5), (37, 250), (64, 256), (100, 517), (257, 241), (300, 1000)]
+SIZES = [(1, 1), (2, 3), (7, 5), (37, 250), (64, 256), (100, 517), (257, 241), (300, 1000), (40, 4096), (33, 4094)]
 
 
 def oracle(n, nx, ny, steps, boundary=0, precision=0, init=0, per=(False, False), **kw):
