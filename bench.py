@@ -1,22 +1,28 @@
-"""Headline benchmark: cell-updates/s of the 5-point Jacobi heat stencil on MI355X.
+"""Headline benchmark: cell-updates/s of the 5-point Jacobi heat stencil on MI355X, with the
+speedup and efficiency over GPUs that the reference's Tables 1-3 report (Report.pdf p.21-22).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched
 by ``torch.distributed.run`` with one rank per GPU.  A "step" is one Jacobi time step of the
 whole grid.  W untimed warm-up steps, then EXACTLY K timed steps bracketed by a barrier and
 ``torch.cuda.synchronize()`` on both sides; the max over ranks is reported by rank 0 as one
-JSON line.
+JSON line.  ``value`` is the whole-job throughput (all GPUs).
 
-Config (BASELINE.json): 4096×4096 fp32 grid, 1000 steps, center-hot initial field
-(synthetic — computed on device from the exact fp64 formula; no dataset involved).
-Numerics: the bit-exact reference expression (fp32 storage, fp64 arithmetic exactly as the
-reference's C evaluates it) unless ``--precision fp32``.
+Default configuration (``--config 4096-strong``, the BASELINE metric): ONE 4096×4096 fp32 grid
+split over the N GPUs (strong scaling; 1-D row strips, the layout whose halos are contiguous
+rows), center-hot initial field computed on device from the exact fp64 formula (synthetic: no
+dataset is involved).  Numerics: the bit-exact reference expression (fp32 storage, fp64
+arithmetic exactly as the reference's C evaluates it) unless ``--precision fp32``.
+Other BASELINE rows: ``--config 8192x2rows``, ``16384x8blocks``, ``weak-4096``, ``weak-hbm``
+(per-GPU tile sized from hipMemGetInfo to fill HBM).
 
-Scaling: ``--scaling weak`` (default) gives every GPU a 4096×4096 tile; ``--scaling strong``
-splits one 4096×4096 grid over the N GPUs.  Decomposition ``--layout rows`` (default): 1-D
-row strips (GRIDX = N, the BASELINE's "1D row decomposition with RCCL ghost-row send/recv"),
-whose few halo-dependent work units run on a second stream CONCURRENTLY with the interior
-while the K-deep ghost rows move over xGMI by RCCL send/recv; ``--layout blocks``: 2-D
-near-square blocks (e.g. 2×4).
+Multi-GPU safety (N > 1): before anything is timed, every candidate (transport, pipeline) —
+the requested one, then safer fallbacks — runs a small grid of the same decomposition and
+must match the CPU oracle bit for bit on rank 0 (``heat2d_amd/utils/benchmark.py``).  The JSON
+says which one passed and what failed.  Speedup/efficiency are measured IN THIS JOB: rank 0
+re-runs the same grid (strong) or one tile (weak) on its GPU alone with the same K and W; for
+strong scaling it also replays the whole step count and compares every rank's tile with the
+single-GPU grid bit for bit (``verified``).
+
 ``vs_baseline`` divides by the reference's best published throughput, 1.01e10 cell-updates/s
 (2560×2048, 160 MPI tasks on 20 nodes, Report.pdf p.21 Table 1 — BASELINE.md).
 """
@@ -31,27 +37,32 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# one hardware queue per engine stream (see heat2d_amd/_native.py); before torch initialises HIP
+# One hardware queue per engine stream (compute and comm must not share one: see
+# heat2d_amd/_native.py).  Read once at HIP initialisation, so it is set before torch starts.
 if os.environ.get("HEAT2D_KEEP_HW_QUEUES") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
-BASELINE_CUPS = 1.01e10
-
 
 def main() -> int:
+    from heat2d_amd.utils.benchmark import CONFIGS
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--side", type=int, default=4096, help="grid side (per GPU for weak scaling)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="4096-strong")
+    ap.add_argument("--side", type=int, default=0, help="override the config's grid side (per GPU for weak)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None, help="override the config's scaling")
+    ap.add_argument("--layout", choices=("rows", "blocks"), default=None, help="override the config's layout")
     ap.add_argument("--precision", choices=("ref", "fp32"), default="ref")
     ap.add_argument("--boundary", choices=("fixed", "ghost-zero"), default="fixed")
     ap.add_argument("--tblock", type=int, default=8)
     ap.add_argument("--rows-per-wave", type=int, default=0)
     ap.add_argument("--transport", choices=("auto", "rccl", "torch", "host"), default="auto")
-    ap.add_argument("--layout", choices=("rows", "blocks"), default="rows")
+    ap.add_argument("--pipeline", choices=("auto", "signal", "concurrent", "boundary-first", "serial"), default="auto")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-gate", action="store_true", help="skip the pre-timing correctness gate (N > 1)")
+    ap.add_argument("--no-reference", action="store_true", help="skip the in-job single-GPU reference run")
     ap.add_argument("--repeat", type=int, default=1, help="timed repetitions (best reported)")
     ap.add_argument("--prewarm-s", type=float, default=0.3,
                     help="seconds of untimed stencil work before the warm-up steps, so the GPU reaches its "
@@ -60,42 +71,92 @@ def main() -> int:
                     help="cpu: rehearsal of the distributed contract on the host (gloo), not a benchmark")
     a = ap.parse_args()
 
+    import numpy as np
     import torch
 
-    from heat2d_amd.config import Config, auto_grid
+    from heat2d_amd._native import native
+    from heat2d_amd.config import Config
     from heat2d_amd.parallel.dist import init_distributed
     from heat2d_amd.solver import Solver
+    from heat2d_amd.utils import benchmark as B
 
     ctx = init_distributed()
     world = ctx.world
     if world != a.gpus and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    gx, gy = (world, 1) if a.layout == "rows" else auto_grid(world)
-    if a.scaling == "weak":
-        nx, ny = a.side * gx, a.side * gy
+    on_gpu = a.device == "gpu"
+    n = native()
+    ndev = n.device_count() if on_gpu else 0
+    if on_gpu and ndev == 0:
+        raise SystemExit("bench: no HIP device (use --device cpu for a host rehearsal)")
+    device = (ctx.local_rank % ndev) if on_gpu else -1
+    ctx.distinct_devices = on_gpu and world <= ndev
+    if on_gpu:
+        torch.cuda.set_device(device)
+
+    bc = B.CONFIGS[a.config]
+    scaling = a.scaling or bc.scaling
+    layout = a.layout or bc.layout
+    side = a.side or bc.side
+    fill_hbm = side == 0
+    if fill_hbm:
+        if not on_gpu:
+            side = 64
+        else:
+            free, _total = n.mem_info(device)
+            side = B.fill_hbm_side(int(ctx.allreduce_min(free)), G=a.tblock)
+    nx, ny, gx, gy = B.grid_for(world, side, scaling, layout)
+
+    def config(nx_, ny_, steps_, transport, pipeline, gridx, gridy):
+        return Config(preset="heat2d", nx=nx_, ny=ny_, steps=steps_, gridx=gridx, gridy=gridy, boundary=a.boundary,
+                      precision=a.precision, init="exact", output="none", device=a.device, transport=transport,
+                      tblock=a.tblock, rows_per_wave=a.rows_per_wave, overlap=not a.no_overlap, pipeline=pipeline,
+                      quiet=True, report="grad", text_style="grad", sync_mode=2)
+
+    # ---- correctness gate + transport/pipeline choice (N > 1) ------------------------------
+    cands = B.candidates(a.transport, a.pipeline, world, on_gpu, ctx.distinct_devices, layout)
+    gate = None
+    if world > 1 and not a.no_gate:
+        bnd = 0 if a.boundary == "fixed" else 1
+        prec = 0 if a.precision == "ref" else 1
+
+        def make_gate_solver(transport, pipeline, gnx, gny, gsteps):
+            c = config(gnx, gny, gsteps, transport, pipeline, gx, gy)
+            c.halo_timeout_s = 5.0
+            return Solver(c, ctx)
+
+        gate = B.run_gate(ctx, make_gate_solver,
+                          lambda gnx, gny, gsteps: n.oracle_run(gnx, gny, gsteps, boundary=bnd, precision=prec)["grid"],
+                          cands, gx, gy, a.tblock, log=lambda m: print(m, file=sys.stderr, flush=True))
+        if not gate.ok:
+            if ctx.rank == 0:
+                print(json.dumps({"error": "no transport passed the correctness gate", "gate": gate.tried}), flush=True)
+            ctx.shutdown()
+            return 3
+        transport, pipeline = gate.transport, gate.pipeline
     else:
-        nx = ny = a.side
-    cfg = Config(preset="heat2d", nx=nx, ny=ny, steps=a.steps, gridx=gx, gridy=gy, boundary=a.boundary,
-                 precision=a.precision, init="exact", output="none", device=a.device, transport=a.transport,
-                 tblock=a.tblock, rows_per_wave=a.rows_per_wave, overlap=not a.no_overlap, quiet=True,
-                 report="grad", text_style="grad")
+        transport, pipeline = cands[0]
+    transport_cfg = "auto" if transport == "local" else transport
+
+    cfg = config(nx, ny, a.steps, transport_cfg, pipeline, gx, gy)
     s = Solver(cfg, ctx)
 
-    on_gpu = a.device == "gpu"
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     def sync_barrier():
-        if on_gpu:
-            torch.cuda.synchronize()
+        sync()
         ctx.barrier()
-        if on_gpu:
-            torch.cuda.synchronize()
+        # device-level alignment (RCCL all-reduce) when every rank has its own GPU
+        if on_gpu and not ctx.device_barrier(device):
+            sync()
 
-    # pre-warm (untimed, time-based) then the W warm-up steps (untimed)
+    # ---- pre-warm (untimed, time-based, collectively agreed count) + W warm-up steps --------
     run = s.run_steps
     prewarm_steps = 0
     if on_gpu and a.prewarm_s > 0:
-        # the batch count is agreed collectively: ranks that ran different step counts would
-        # post unmatched halo sends/receives and deadlock
+        # ranks that ran different step counts would post unmatched halo sends and deadlock
         sync_barrier()
         t0 = time.perf_counter()
         run(64)
@@ -107,24 +168,70 @@ def main() -> int:
         sync_barrier()
     if a.warmup > 0:
         run(a.warmup)
-    best = None
-    res = None
-    times = []
+
+    # ---- timed region -----------------------------------------------------------------------
+    best, res, times = None, None, []
     for _ in range(max(1, a.repeat)):
         sync_barrier()
         t0 = time.perf_counter()
         res = run(a.steps)
-        sync_barrier()
+        sync()
         dt = ctx.allreduce_max(time.perf_counter() - t0)
         times.append(dt)
         best = dt if best is None else min(best, dt)
-    expect = prewarm_steps + max(0, a.warmup) + a.steps * max(1, a.repeat)
-    if res["steps_done"] != expect:
-        raise SystemExit(f"bench: step accounting error ({res['steps_done']} != {expect})")
+    total_steps = prewarm_steps + max(0, a.warmup) + a.steps * max(1, a.repeat)
+    if res["steps_done"] != total_steps:
+        raise SystemExit(f"bench: step accounting error ({res['steps_done']} != {total_steps})")
     cups = float(nx) * float(ny) * a.steps / best
+    pipeline_used = s.engine.pipeline()
+    halo_depth = s.engine.halo_depth()
+    path = res["path"]
+
+    # ---- in-job single-GPU reference: speedup / efficiency, and bit-exact verification ------
+    t1 = None
+    verified = None
+    ref_note = None
+    if world == 1:
+        t1 = best
+    elif not a.no_reference and not fill_hbm:
+        # strong: the same global grid on rank 0's GPU alone; weak: one GPU's tile alone
+        rnx, rny = (nx, ny) if scaling == "strong" else (side, side)
+        digests = ctx.gather_objects(B.grid_digest(s.tiles()) if scaling == "strong" else None)
+        if ctx.rank == 0:
+            e = n.Engine(rnx, rny, boundary=0 if a.boundary == "fixed" else 1,
+                         precision=0 if a.precision == "ref" else 1, tblock=a.tblock,
+                         rows_per_wave=a.rows_per_wave, device=device, small_grid_lds=False)
+            pre = prewarm_steps + max(0, a.warmup)
+            e.run(pre) if pre > 0 else None
+            ts = []
+            for _ in range(max(1, a.repeat)):
+                e.synchronize()
+                t0 = time.perf_counter()
+                e.run(a.steps)
+                e.synchronize()
+                ts.append(time.perf_counter() - t0)
+            t1 = min(ts)
+            if scaling == "strong":
+                full = e.download(0)
+                verified = all(B.digest_of_region(full, k) == v for d in digests for k, v in d.items())
+            ref_note = (f"rank 0's GPU alone, {'same grid' if scaling == 'strong' else 'one tile'}, "
+                        f"same K/W, measured in this job")
+            del e
+        ctx.barrier()
+
+    # ---- report ---------------------------------------------------------------------------------
     if ctx.rank == 0:
+        if t1 is not None:
+            if scaling == "strong":
+                speedup = t1 / best
+                eff = speedup / world
+            else:  # weak: each GPU does the work of the 1-GPU run
+                eff = t1 / best
+                speedup = eff * world
+        else:
+            speedup = eff = None
         out = {
-            "metric": "cell-updates/sec (whole node), 4096^2 grid 1000 steps",
+            "metric": B.metric_label(nx, ny, a.steps),
             "value": cups,
             "unit": "cell-updates/s",
             "n_gpus": world,
@@ -132,25 +239,34 @@ def main() -> int:
             "warmup": a.warmup,
             "ms_per_step": best * 1e3 / a.steps,
             "higher_is_better": True,
-            "scaling": a.scaling,
-            "vs_baseline": cups / BASELINE_CUPS,
+            "scaling": scaling,
+            "vs_baseline": cups / B.BASELINE_CUPS,
+            "speedup": speedup,
+            "efficiency": eff,
+            "t1_ms_per_step": (t1 * 1e3 / a.steps) if t1 is not None else None,
+            "speedup_reference": ref_note or ("this run (N=1)" if world == 1 else None),
+            "verified": verified,
             "dtype": "fp32",
             "compute": ("fp64 expression, bit-exact with the reference" if a.precision == "ref" else "fp32 FMA"),
             "data": "synthetic center-hot initial field (exact formula, generated on device)",
             "elapsed_s": best,
             "repeats_s": times,
             "prewarm_steps": prewarm_steps,
+            "gate": (gate.tried if gate is not None else None),
             "config": {
-                "model": "heat2d 5-point Jacobi, fixed edges" if a.boundary == "fixed" else "heat2d 5-point Jacobi, zero ghost ring",
+                "name": a.config,
+                "model": ("heat2d 5-point Jacobi, fixed edges" if a.boundary == "fixed"
+                          else "heat2d 5-point Jacobi, zero ghost ring"),
                 "grid": [nx, ny],
                 "grid_per_gpu": [nx // gx, ny // gy],
                 "global_batch": nx * ny,
                 "seq_len": a.steps,
-                "parallelism": (f"rows{gx}" if a.layout == "rows" else f"blocks{gx}x{gy}") if world > 1 else "single",
-                "overlap": s.engine.pipeline(),
-                "tblock": s.engine.halo_depth(),
-                "path": res["path"],
-                "transport": cfg.transport,
+                "parallelism": B.parallelism_label(world, gx, gy),
+                "transport": transport,
+                "pipeline": pipeline_used,
+                "tblock": halo_depth,
+                "path": path,
+                "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             },
         }
         print(json.dumps(out), flush=True)

@@ -46,6 +46,9 @@ class Config:
     tblock: int = 8
     rows_per_wave: int = 0
     overlap: bool = True
+    pipeline: str = "auto"  # auto | signal | concurrent | boundary-first | serial (multi-rank halo pipeline)
+    sync_mode: int = 0  # end-of-run synchronisation (EngineOptions::sync_mode; the bench uses 2)
+    halo_timeout_s: float = 30.0  # bounded device-side halo waits give up (and the run fails) after this
     small_grid: bool = True
     tiled: str = "auto"  # auto | on | off: LDS-tiled temporally-blocked kernel (single-tile small/medium grids)
     naive: bool = False
@@ -126,6 +129,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--tblock", type=int, default=8, help="time steps fused per kernel (halo depth)")
     p.add_argument("--rows-per-wave", type=int, default=0, help="rows per wave work unit (0 = auto)")
     p.add_argument("--no-overlap", action="store_true", help="do not overlap halo exchange with interior compute")
+    p.add_argument("--pipeline", choices=("auto", "signal", "concurrent", "boundary-first", "serial"), default="auto",
+                   help="multi-rank halo pipeline (auto: the transport's default)")
     p.add_argument("--no-small-grid", action="store_true", help="disable the whole-grid LDS solver")
     p.add_argument("--tiled", choices=("auto", "on", "off"), default="auto",
                    help="LDS-tiled temporally-blocked kernel for single-tile small/medium grids")
@@ -173,6 +178,7 @@ def config_from_args(argv: Optional[Sequence[str]] = None) -> Config:
         tblock=a.tblock,
         rows_per_wave=a.rows_per_wave,
         overlap=not a.no_overlap,
+        pipeline=a.pipeline,
         small_grid=not a.no_small_grid,
         tiled=a.tiled,
         naive=a.naive,

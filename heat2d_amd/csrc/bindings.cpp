@@ -6,6 +6,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -142,6 +143,37 @@ py::dict device_props(int dev) {
   return d;
 }
 
+// EngineOptions fields settable by keyword from Python (Engine(nx, ny, **kw)).  One line per
+// option; an unknown keyword is an error (no silently ignored typos).
+using OptSetter = std::function<void(EngineOptions&, const py::handle&)>;
+const std::map<std::string, OptSetter>& engine_option_table() {
+#define H2D_OPT(name) {#name, [](EngineOptions& o, const py::handle& v) { o.name = v.cast<decltype(o.name)>(); }}
+  static const std::map<std::string, OptSetter> t = {
+      H2D_OPT(gridx), H2D_OPT(gridy), H2D_OPT(periodic_x), H2D_OPT(periodic_y), H2D_OPT(boundary),
+      H2D_OPT(precision), H2D_OPT(init), H2D_OPT(cx), H2D_OPT(cy), H2D_OPT(tblock), H2D_OPT(rows_per_wave),
+      H2D_OPT(edge_weight), H2D_OPT(wave_capacity), H2D_OPT(boundary_rows), H2D_OPT(concurrent),
+      H2D_OPT(comm_boundary), H2D_OPT(signal_exchange), H2D_OPT(device_halo_wait), H2D_OPT(comm_priority),
+      H2D_OPT(signal_plan), H2D_OPT(watchdog_s), H2D_OPT(halo_timeout_s), H2D_OPT(sync_mode), H2D_OPT(trace), H2D_OPT(poison), H2D_OPT(convergence),
+      H2D_OPT(interval), H2D_OPT(sensitivity), H2D_OPT(device), H2D_OPT(ranks), H2D_OPT(transport),
+      H2D_OPT(overlap), H2D_OPT(small_grid_lds), H2D_OPT(tiled), H2D_OPT(tile_rows), H2D_OPT(tile_width),
+      H2D_OPT(tile_k), H2D_OPT(naive), H2D_OPT(comm_cus), H2D_OPT(comm_cu_layout), H2D_OPT(reserve_waves),
+      H2D_OPT(device_fence_events), H2D_OPT(contiguous_halo),
+  };
+#undef H2D_OPT
+  return t;
+}
+
+void apply_engine_options(EngineOptions& o, const py::kwargs& kw) {
+  const auto& t = engine_option_table();
+  for (auto item : kw) {
+    const std::string k = item.first.cast<std::string>();
+    auto it = t.find(k);
+    if (it == t.end()) throw py::type_error("Engine: unknown option '" + k + "'");
+    if (item.second.is_none()) continue;
+    it->second(o, item.second);
+  }
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_heat2d, m) {
@@ -255,70 +287,21 @@ PYBIND11_MODULE(_heat2d, m) {
 
   // ---- engine -----------------------------------------------------------------------------
   py::class_<Engine>(m, "Engine")
-      .def(py::init([](int64_t nx, int64_t ny, int gridx, int gridy, bool per_x, bool per_y, int boundary,
-                       int precision, int init, double cx, double cy, int tblock, int rows_per_wave, bool convergence,
-                       int64_t interval, double sensitivity, int device, std::vector<int> ranks, int transport,
-                       bool overlap, bool small_grid_lds, bool naive, double edge_weight, int64_t wave_capacity, int concurrent, int boundary_rows, double watchdog_s, bool trace, bool poison,
-                       int comm_cus, int contiguous_halo, int comm_cu_layout, int reserve_waves,
-                       bool device_fence_events, int comm_boundary, int signal_exchange, int device_halo_wait, int tiled, int tile_rows, int tile_width, int tile_k, int comm_priority, int signal_plan) {
+      .def(py::init([](int64_t nx, int64_t ny, py::kwargs kw) {
              EngineOptions o;
              o.nx = nx;
              o.ny = ny;
-             o.gridx = gridx;
-             o.gridy = gridy;
-             o.periodic_x = per_x;
-             o.periodic_y = per_y;
-             o.boundary = boundary;
-             o.precision = precision;
-             o.init = init;
-             o.cx = cx;
-             o.cy = cy;
-             o.tblock = tblock;
-             o.rows_per_wave = rows_per_wave;
-             o.convergence = convergence;
-             o.interval = interval;
-             o.sensitivity = sensitivity;
-             o.device = device;
-             o.ranks = ranks;
-             o.transport = transport;
-             o.overlap = overlap;
-             o.small_grid_lds = small_grid_lds;
-             o.naive = naive;
-             o.edge_weight = edge_weight;
-             o.wave_capacity = wave_capacity;
-             o.concurrent = concurrent;
-             o.boundary_rows = boundary_rows;
-             o.watchdog_s = watchdog_s;
-             o.trace = trace;
-             o.poison = poison;
-             o.comm_cus = comm_cus;
-             o.contiguous_halo = contiguous_halo;
-             o.comm_cu_layout = comm_cu_layout;
-             o.reserve_waves = reserve_waves;
-             o.device_fence_events = device_fence_events;
-             o.comm_boundary = comm_boundary;
-             o.signal_exchange = signal_exchange;
-             o.device_halo_wait = device_halo_wait;
-             o.tiled = tiled;
-             o.tile_rows = tile_rows;
-             o.tile_width = tile_width;
-             o.tile_k = tile_k;
-             o.comm_priority = comm_priority;
-             o.signal_plan = signal_plan;
+             apply_engine_options(o, kw);
+             py::gil_scoped_release nogil;
              return new Engine(o);
            }),
-           py::arg("nx"), py::arg("ny"), py::arg("gridx") = 1, py::arg("gridy") = 1, py::arg("periodic_x") = false,
-           py::arg("periodic_y") = false, py::arg("boundary") = (int)kFixed, py::arg("precision") = (int)kRef,
-           py::arg("init") = (int)kInitExact, py::arg("cx") = kCxDouble, py::arg("cy") = kCxDouble,
-           py::arg("tblock") = 8, py::arg("rows_per_wave") = 0, py::arg("convergence") = false,
-           py::arg("interval") = 20, py::arg("sensitivity") = 0.1, py::arg("device") = 0,
-           py::arg("ranks") = std::vector<int>{}, py::arg("transport") = (int)kTransportAuto,
-           py::arg("overlap") = true, py::arg("small_grid_lds") = true, py::arg("naive") = false,
-           py::arg("edge_weight") = 1.2, py::arg("wave_capacity") = 0, py::arg("concurrent") = -1, py::arg("boundary_rows") = 8,
-           py::arg("watchdog_s") = 900.0, py::arg("trace") = false, py::arg("poison") = false,
-           py::arg("comm_cus") = -1, py::arg("contiguous_halo") = -1, py::arg("comm_cu_layout") = 0, py::arg("reserve_waves") = -1,
-           py::arg("device_fence_events") = false, py::arg("comm_boundary") = -1, py::arg("signal_exchange") = -1, py::arg("device_halo_wait") = -1,
-           py::arg("tiled") = -1, py::arg("tile_rows") = 0, py::arg("tile_width") = 0, py::arg("tile_k") = 0, py::arg("comm_priority") = -1, py::arg("signal_plan") = -1)
+           py::arg("nx"), py::arg("ny"),
+           "Engine(nx, ny, **options): every EngineOptions field by name (see engine.h)")
+      .def_static("option_names", []() {
+        std::vector<std::string> v;
+        for (auto& kv : engine_option_table()) v.push_back(kv.first);
+        return v;
+      })
       .def("num_tiles", &Engine::num_tiles)
       .def("tile_rank", &Engine::tile_rank)
       .def("geom", [](const Engine& e, int t) { return geom_dict(e.geom(t)); })
@@ -406,6 +389,15 @@ PYBIND11_MODULE(_heat2d, m) {
   // ---- devices -----------------------------------------------------------------------------
   m.def("device_count", &device_count);
   m.def("device_props", &device_props);
+  m.def(
+      "mem_info",
+      [](int dev) {
+        size_t fr = 0, tot = 0;
+        H2D_HIP_CHECK(hipSetDevice(dev));
+        H2D_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+        return py::make_tuple((int64_t)fr, (int64_t)tot);
+      },
+      py::arg("device") = 0, "(free, total) device memory in bytes (hipMemGetInfo)");
 
   // ---- raw-pointer kernel ops (torch tensors laid out as TileGeom storage) ---------------
   m.def(

@@ -153,6 +153,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, evf));
     H2D_HIP_CHECK(hipEventCreate(&ev_t0_));
     H2D_HIP_CHECK(hipEventCreate(&ev_t1_));
+    H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
     d_resid_ = dmalloc<double>(ranks.size() + 1);
     H2D_HIP_CHECK(hipHostMalloc(&h_resid_, sizeof(double) * (ranks.size() + 1)));
     d_lds_steps_ = dmalloc<long long>(1);
@@ -215,6 +216,9 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       H2D_HIP_CHECK(hipMemset(sig_counter_, 0, sizeof(unsigned long long)));
       d_sig_timeout_ = dmalloc<unsigned int>(1);
       H2D_HIP_CHECK(hipMemset(d_sig_timeout_, 0, sizeof(unsigned int)));
+      H2D_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_timeout_), sizeof(unsigned int), hipHostMallocMapped));
+      *h_timeout_ = 0u;
+      H2D_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_timeout_dev_), h_timeout_, 0));
       dev_wait_ = opt_.device_halo_wait != 0;
       if (dev_wait_) {
         halo_counter_ = dmalloc<unsigned long long>(8);
@@ -291,6 +295,8 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
         }
       }
     }
+    if (!opt_.naive) warm_stream_kernels(opt_.precision, G_, compute_);
+    if (tiled_) warm_tile_kernels(opt_.precision, compute_);
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
   }
 }
@@ -312,6 +318,7 @@ Engine::~Engine() {
   }
   hipFree(sig_counter_);
   hipFree(d_sig_timeout_);
+  if (h_timeout_) hipHostFree(h_timeout_);
   hipFree(halo_counter_);
   for (auto* m : {&local_descs_, &pack_descs_, &unpack_descs_})
     for (auto& kv : *m) hipFree(std::get<0>(kv.second));
@@ -326,6 +333,7 @@ Engine::~Engine() {
   hipEventDestroy(ev_halo_);
   hipEventDestroy(ev_t0_);
   hipEventDestroy(ev_t1_);
+  hipEventDestroy(ev_done_);
   if (bstream_) hipStreamDestroy(bstream_);
   for (int i = 0; i < 2; ++i) {
     if (ev_i_[i]) hipEventDestroy(ev_i_[i]);
@@ -370,8 +378,11 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   bool peer[kNumDirs];
   for (int d = 0; d < kNumDirs; ++d) peer[d] = dec_.neighbor(tl.rank, d) >= 0;
   const int64_t cap = wave_capacity(K);
+  // Halo-dependent units gate the exchange of the NEXT chunk, which may be up to G_ rows deep
+  // whatever this chunk's K: they must cover (and release) at least G_ rows.
+  const int hb = std::max(opt_.boundary_rows, G_);
   UnitPlan P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
-                          opt_.edge_weight, cap, peer, opt_.boundary_rows);
+                          opt_.edge_weight, cap, peer, hb);
   // auto headroom (4096^2 row-periodic RCCL self-exchange, us/step: 14.3 -> 10.4-10.9 with
   // 16 in the concurrent pipeline; 14.3 -> 12.6 with 32 in the boundary-first one)
   const int64_t reserve = opt_.reserve_waves >= 0 ? opt_.reserve_waves : ((concurrent_ || sig_mode_ > 0) ? 16 : 32);
@@ -381,7 +392,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     const int64_t nb = (concurrent_ || sig_mode_ > 0) ? (int64_t)P.boundary.size() : 0;
     const int64_t cap_in = std::max<int64_t>(cap / 2, cap - nb - reserve);
     P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
-                   opt_.edge_weight, cap_in, peer, opt_.boundary_rows);
+                   opt_.edge_weight, cap_in, peer, hb);
   }
   // Signalled pipeline with only north/south peers (1-D row strips): no short boundary units.
   // Every strip is cut into capacity-fitted units as if the tile had no peers; the top unit
@@ -395,7 +406,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   if (sig_mode_ > 0 && opt_.overlap && has_exchange_ && ns_only && (peer[kN] || peer[kS]) && opt_.signal_plan != 0) {
     const int64_t reserve_sig = opt_.reserve_waves >= 0 ? opt_.reserve_waves : 16;
     UnitPlan Q = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
-                            opt_.edge_weight, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, opt_.boundary_rows);
+                            opt_.edge_weight, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, hb);
     std::map<int, std::pair<int, int>> ends;  // strip -> (top unit, bottom unit) indices
     for (int i = 0; i < (int)Q.interior.size(); ++i) {
       const Unit& u = Q.interior[i];
@@ -413,8 +424,10 @@ const Engine::UnitLists& Engine::units(int t, int K) {
       }
       if (peer[kN]) role[ti] = 1;
       if (peer[kS]) role[bi] = 2;
-      // the neighbouring units' K-cones must not reach the ghost rows
-      if ((peer[kN] && Q.interior[ti].h < K) || (peer[kS] && Q.interior[bi].h < K)) ok = false;
+      // the neighbouring units' K-cones must not reach the ghost rows, and a signalling unit
+      // must own every row the next exchange sends (up to G_, whatever this chunk's K)
+      if ((peer[kN] && Q.interior[ti].h < std::max(K, G_)) || (peer[kS] && Q.interior[bi].h < std::max(K, G_)))
+        ok = false;
     }
     if (ok) {
       std::vector<Unit> sg, rest;
@@ -430,7 +443,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
       }
       P.interior = rest;
       P.boundary = sg;
-      L.sig_rows = K;
+      L.sig_rows = G_;  // released rows cover the deepest exchange that can follow
     }
   }
   std::vector<Unit>& in = P.interior;
@@ -512,8 +525,10 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     if (dev_wait_) {
       a.halo_ready = halo_counter_;
       a.halo_need = halo_seq_;
-      a.halo_polls = 20000000LL;  // ~1-2 us per system-scope poll: gives up after tens of seconds
+      // ~1-2 us per system-scope poll (s_sleep 2 between polls)
+      a.halo_polls = std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6));
       a.timed_out = d_sig_timeout_;
+      a.timed_out_host = h_timeout_dev_;
     }
   }
   launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
@@ -530,18 +545,21 @@ int Engine::chunk_len(int64_t done, int64_t total, int kmax, bool* check) const 
   // A chunk never crosses a convergence check; the check step is a chunk of its own, so a
   // converged run can roll back exactly one step (B-5 semantics).
   *check = false;
-  const int64_t remaining = total - done;
-  if (remaining <= 0) return 0;
-  int64_t k = std::min<int64_t>(kmax, remaining);
+  int64_t seg = total - done;  // steps up to the end of the run or the next check step
+  if (seg <= 0) return 0;
   if (opt_.convergence) {
     const int64_t next_check = (done / opt_.interval + 1) * opt_.interval;
     if (done + 1 == next_check) {
       *check = true;
       return 1;
     }
-    k = std::min<int64_t>(k, next_check - 1 - done);
+    seg = std::min<int64_t>(seg, next_check - 1 - done);
   }
-  return (int)std::max<int64_t>(1, k);
+  // Balanced chunks: a segment of L steps runs as ceil(L/kmax) launches of near-equal depth
+  // (20 steps at K<=8: 7+7+6, not 8+8+4 — a launch's makespan is set by its deepest units, so a
+  // ragged tail costs nearly a full launch of fixed overhead for half the work).
+  const int64_t n = (seg + kmax - 1) / kmax;
+  return (int)std::max<int64_t>(1, (seg + n - 1) / n);
 }
 
 int Engine::next_chunk(int64_t done, int64_t total, bool* check) const {
@@ -697,8 +715,9 @@ void Engine::gate_exchange() {
   if (sig_mode_ == 1) {
     H2D_HIP_CHECK(hipStreamWaitValue64(comm_, sig_counter_, sig_target_, hipStreamWaitValueGte));
   } else {
-    // ~0.5 us per poll: gives up after ~30 s (reported at the end of the run)
-    launch_wait_counter(sig_counter_, sig_target_, d_sig_timeout_, 60000000LL, comm_);
+    // ~0.5 us per poll: gives up after ~halo_timeout_s (polled by the host per chunk)
+    launch_wait_counter(sig_counter_, sig_target_, d_sig_timeout_, h_timeout_dev_,
+                        std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 2e6)), comm_);
   }
 }
 
@@ -765,6 +784,10 @@ void Engine::wait_event(hipEvent_t ev) {
   // Failure detection: with a communicator, poll the event and RCCL's asynchronous error
   // state instead of blocking, and abort the communicator after `watchdog_s` without
   // completion (a dead peer would otherwise hang the rank forever).
+  if (!ev) {
+    H2D_HIP_CHECK(hipEventRecord(ev_done_, compute_));
+    ev = ev_done_;
+  }
   if (!rccl_comm_) {
     H2D_HIP_CHECK(hipEventSynchronize(ev));
     return;
@@ -815,7 +838,24 @@ RunStats Engine::run(int64_t steps) {
   }
 }
 
+void Engine::poll_abort() {
+  if (!h_timeout_) return;
+  const unsigned int to = __atomic_load_n(h_timeout_, __ATOMIC_ACQUIRE);
+  if (!to) return;
+  // The device gave up on a halo: every later chunk computes on stale ghost cells and the
+  // host's sig/halo sequence numbers no longer match the device counters, so this engine
+  // cannot be reused.  Drain what is queued (bounded waits: it terminates).
+  broken_ = true;
+  broken_why_ = std::string("signalled halo pipeline timed out: ") +
+                ((to & 1) ? "the exchange gate (boundary units never completed) " : "") +
+                ((to & 2) ? "the device-side halo wait (the exchange never landed)" : "");
+  hipStreamSynchronize(comm_);
+  hipStreamSynchronize(compute_);
+  throw std::runtime_error(broken_why_);
+}
+
 RunStats Engine::run_impl(int64_t steps) {
+  if (broken_) throw std::runtime_error("engine unusable after an earlier failure: " + broken_why_);
   if (transport_ == kTransportExternal && has_exchange_)
     throw std::runtime_error("external transport: drive the loop from the caller");
   if (transport_ == kTransportRccl && has_exchange_ && !rccl_comm_)
@@ -850,7 +890,8 @@ RunStats Engine::run_impl(int64_t steps) {
     return st;
   }
 
-  H2D_HIP_CHECK(hipEventRecord(ev_t0_, compute_));
+  const bool timing = opt_.sync_mode == 0 || opt_.sync_mode == 3;
+  if (timing) H2D_HIP_CHECK(hipEventRecord(ev_t0_, compute_));
   const bool single = tiles_.size() == 1 && !has_exchange_;
   if (tiled_) {
     // LDS-tiled path: one launch per chunk of up to tile_k_ steps, the tiling re-derived per
@@ -892,7 +933,6 @@ RunStats Engine::run_impl(int64_t steps) {
       }
       steps_done_ += k;
     }
-    H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
   } else if (single && opt_.small_grid_lds && !opt_.naive && lds_solver_fits(dec_.NX, dec_.NY) && steps > 0) {
     // Whole run inside one workgroup's LDS.
     st.path = "lds";
@@ -904,7 +944,6 @@ RunStats Engine::run_impl(int64_t steps) {
     launch_lds_solver(T.buf[T.cur] + T.g.idx(0, 0), T.g.pitch, T.buf[1 - T.cur] + T.g.idx(0, 0), T.g.pitch, T.g.xcell,
                       T.g.ycell, steps, opt_.precision, opt_.boundary, opt_.cx, opt_.cy, opt_.periodic_x,
                       opt_.periodic_y, interval, opt_.sensitivity, d_lds_steps_, d_resid_, compute_);
-    H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
     long long done = 0;
     H2D_HIP_CHECK(hipMemcpyAsync(&done, d_lds_steps_, sizeof(long long), hipMemcpyDeviceToHost, compute_));
     H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, sizeof(double), hipMemcpyDeviceToHost, compute_));
@@ -946,6 +985,7 @@ RunStats Engine::run_impl(int64_t steps) {
         trace_end("chunk", compute_);
         for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
         ++st.chunks;
+        poll_abort();
         bool check_next = false;
         const int k_next = next_chunk(steps_done_ + k, target, &check_next);
         if (check) {
@@ -1182,26 +1222,39 @@ RunStats Engine::run_impl(int64_t steps) {
         steps_done_ += k;
       }
     }
-    H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
   }
-  wait_event(ev_t1_);
-  if (d_sig_timeout_) {
-    unsigned int to = 0;
-    H2D_HIP_CHECK(hipMemcpy(&to, d_sig_timeout_, sizeof(to), hipMemcpyDeviceToHost));
-    if (to) {
-      H2D_HIP_CHECK(hipMemset(d_sig_timeout_, 0, sizeof(unsigned int)));
-      throw std::runtime_error(std::string("signalled halo pipeline timed out: ") +
-                               ((to & 1) ? "the exchange gate (boundary units never completed) " : "") +
-                               ((to & 2) ? "the device-side halo wait (the exchange never landed)" : ""));
+  end_of_run_wait(st, w0);
+  poll_abort();
+  trace_collect(st);
+  st.steps_done = steps_done_;
+  return st;
+}
+
+void Engine::end_of_run_wait(RunStats& st, std::chrono::steady_clock::time_point w0) {
+  // Everything of the run is on compute_ (the pipelines join the other streams into it).
+  const int m = opt_.sync_mode;
+  if (m == 0 || m == 3) H2D_HIP_CHECK(hipEventRecord(ev_t1_, compute_));
+  if (m == 1) H2D_HIP_CHECK(hipEventRecord(ev_done_, compute_));
+  if (rccl_comm_ || m == 0) {
+    wait_event(m == 1 ? ev_done_ : m == 2 ? nullptr : ev_t1_);
+  } else if (m == 2) {
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+  } else {
+    hipEvent_t ev = m == 1 ? ev_done_ : ev_t1_;
+    for (;;) {  // spin: no interrupt / yield wake-up latency on the critical path of a short run
+      const hipError_t e = hipEventQuery(ev);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) H2D_HIP_CHECK(e);
     }
   }
-  trace_collect(st);
-  float ms = 0.0f;
-  H2D_HIP_CHECK(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
-  st.device_ms = ms;
-  st.steps_done = steps_done_;
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
-  return st;
+  if (m == 0 || m == 3) {
+    float ms = 0.0f;
+    H2D_HIP_CHECK(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
+    st.device_ms = ms;
+  } else {
+    st.device_ms = st.wall_ms;
+  }
 }
 
 int64_t Engine::send_count(int t, int k) const {

@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <map>
 #include <memory>
 #include <string>
@@ -70,6 +71,13 @@ struct EngineOptions {
   // signalled pipeline unit plan for 1-D row strips: -1/1 full-size signalling units (mid-unit
   // signal, bottom units streamed bottom-up), 0 short boundary units (signal at their end)
   int signal_plan = -1;
+  // Bounded device-side waits (halo wait in the stencil, exchange gate) give up after about
+  // this long, report it, and the run fails instead of hanging the queue.
+  double halo_timeout_s = 30.0;
+  // End-of-run synchronisation (the fixed cost of a short timed run): 0 hipEvent timing pair +
+  // hipEventSynchronize; 1 no timing pair, spin on one untimed completion event; 2 no events,
+  // hipStreamSynchronize; 3 timing pair, spin on the end event.  device_ms is wall time in 1/2.
+  int sync_mode = 0;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
   bool poison = false;        // debug canary: NaN in every cell no valid update may read
@@ -226,7 +234,8 @@ class Engine {
   hipStream_t compute_ = nullptr, comm_ = nullptr, bstream_ = nullptr;
   hipEvent_t ev_i_[2] = {nullptr, nullptr}, ev_b_[2] = {nullptr, nullptr};
   bool concurrent_ = false;
-  hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_t0_ = nullptr, ev_t1_ = nullptr;
+  hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_t0_ = nullptr, ev_t1_ = nullptr, ev_done_ = nullptr;
+  void end_of_run_wait(RunStats& st, std::chrono::steady_clock::time_point w0);
   std::map<std::pair<int, int>, UnitLists> units_;
   std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> local_descs_;  // (K, parity)
   std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> pack_descs_;   // (K, parity) for rccl
@@ -245,7 +254,12 @@ class Engine {
   int sig_mode_ = 0;                        // resolved signal_exchange
   unsigned long long* sig_counter_ = nullptr;  // boundary units completed (cumulative)
   unsigned long long sig_target_ = 0;          // boundary units launched (cumulative, host)
-  unsigned int* d_sig_timeout_ = nullptr;
+  unsigned int* d_sig_timeout_ = nullptr;      // bounded waits that gave up (device word, fail-fast)
+  unsigned int* h_timeout_ = nullptr;          // its host-mapped mirror, polled per chunk
+  unsigned int* h_timeout_dev_ = nullptr;      // device view of h_timeout_
+  bool broken_ = false;                        // a wait timed out: halos and counters are out of step
+  std::string broken_why_;
+  void poll_abort();                           // throw (and mark broken) if a device wait gave up
   bool dev_wait_ = false;                      // resolved device_halo_wait
   unsigned long long* halo_counter_ = nullptr;  // exchanges landed (cumulative)
   unsigned long long halo_seq_ = 0;            // exchanges enqueued (cumulative, host)

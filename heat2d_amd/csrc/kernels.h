@@ -98,6 +98,7 @@ struct StreamArgs {
   unsigned long long halo_need = 0;
   long long halo_polls = 0;
   unsigned int* timed_out = nullptr;
+  unsigned int* timed_out_host = nullptr;  // host-mapped mirror of *timed_out (polled by the host per chunk)
 };
 
 // Largest K with a compiled streaming kernel.
@@ -105,6 +106,9 @@ constexpr int kMaxK = 16;
 bool stream_k_supported(int K);
 
 void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hipStream_t s);
+// No-op launches of every compiled streaming kernel with K <= kmax (both residual variants of
+// `precision`), so that no code object is first loaded inside a timed run (one TU per K).
+void warm_stream_kernels(int precision, int kmax, hipStream_t s);
 void launch_naive_step(const TileGeom& g, const float* src, float* dst, int precision, int boundary, double cx,
                        double cy, bool per_x, bool per_y, hipStream_t s);
 void launch_init(const TileGeom& g, float* base, int init, hipStream_t s);
@@ -114,7 +118,7 @@ void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s);
 // One wave polls *counter (system-scope acquire loads, s_sleep between polls) until it reaches
 // `target`; after `max_polls` it gives up and sets *timed_out (the caller reports it).
 void launch_wait_counter(const unsigned long long* counter, unsigned long long target, unsigned int* timed_out,
-                         long long max_polls, hipStream_t s);
+                         unsigned int* timed_out_host, long long max_polls, hipStream_t s);
 // *counter = value with a system-scope release, once every earlier command on `s` is done.
 void launch_set_counter(unsigned long long* counter, unsigned long long value, hipStream_t s);
 // Residual of a whole tile (Σ (a-b)² over owned cells) — used by tests/ops.

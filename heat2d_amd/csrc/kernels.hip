@@ -72,7 +72,8 @@ __global__ __launch_bounds__(256) void reduce_sum_kernel(const double* __restric
 // boundary-unit counter with system-scope acquire loads.  Bounded: a gate that never opens
 // reports a timeout instead of hanging the queue.
 __global__ __launch_bounds__(64) void wait_counter_kernel(const unsigned long long* counter, unsigned long long target,
-                                                          unsigned int* timed_out, long long max_polls) {
+                                                          unsigned int* timed_out, unsigned int* timed_out_host,
+                                                          long long max_polls) {
   if (threadIdx.x != 0) return;
   if (__hip_atomic_load(timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;  // fail fast
   for (long long i = 0; i < max_polls; ++i) {
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(64) void wait_counter_kernel(const unsigned long lo
     if (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= target) return;
     __builtin_amdgcn_s_sleep(4);
   }
-  __hip_atomic_fetch_or(timed_out, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  report_timeout(timed_out, timed_out_host, 1u);
 }
 
 __global__ __launch_bounds__(64) void set_counter_kernel(unsigned long long* counter, unsigned long long value) {
@@ -415,6 +416,24 @@ void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hip
   H2D_HIP_CHECK(hipGetLastError());
 }
 
+void warm_stream_kernels(int precision, int kmax, hipStream_t s) {
+  StreamArgs a{};
+  a.nunits = 0;
+  const bool f32 = precision == kFp32;
+  for (int K = 1; K <= std::min(kmax, kMaxK); ++K) {
+    if (!stream_k_supported(K)) continue;
+    for (bool resid : {false, true}) {
+      switch (K) {
+#define H2D_CASE(KK) case KK: launch_stream_k<KK>(a, f32, resid, s); break;
+        H2D_K_LIST(H2D_CASE)
+#undef H2D_CASE
+        default: break;
+      }
+    }
+  }
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
 void launch_naive_step(const TileGeom& g, const float* src, float* dst, int precision, int boundary, double cx,
                        double cy, bool per_x, bool per_y, hipStream_t s) {
   if (g.xcell <= 0 || g.ycell <= 0) return;
@@ -455,8 +474,9 @@ void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s) {
 }
 
 void launch_wait_counter(const unsigned long long* counter, unsigned long long target, unsigned int* timed_out,
-                         long long max_polls, hipStream_t s) {
-  hipLaunchKernelGGL(wait_counter_kernel, dim3(1), dim3(64), 0, s, counter, target, timed_out, max_polls);
+                         unsigned int* timed_out_host, long long max_polls, hipStream_t s) {
+  hipLaunchKernelGGL(wait_counter_kernel, dim3(1), dim3(64), 0, s, counter, target, timed_out, timed_out_host,
+                     max_polls);
   H2D_HIP_CHECK(hipGetLastError());
 }
 

@@ -239,6 +239,14 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, int64_
   if (sig_at >= ir0) unit_signal(sig, lane);
 }
 
+// A bounded wait gave up: set `bit` in the device word (fail-fast for later waits) and in its
+// host-mapped mirror (a plain system-scope store: no PCIe atomic needed), which the host polls
+// per chunk to abort the run early instead of computing on with stale halos.
+__device__ __forceinline__ void report_timeout(unsigned int* dev, unsigned int* host, unsigned int bit) {
+  if (dev) __hip_atomic_fetch_or(dev, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (host) __hip_atomic_store(host, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -266,7 +274,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
       // relaxed polls (an acquire per poll is 2-3x slower per hop), ONE acquire after the match
       while (__hip_atomic_load(a.halo_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.halo_need) {
         if (++i > a.halo_polls) {
-          __hip_atomic_fetch_or(a.timed_out, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          report_timeout(a.timed_out, a.timed_out_host, 2u);
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
 
 template <int K>
 void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s) {
-  const int blocks = (a.nunits + 3) / 4;
+  const int blocks = std::max(1, (a.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_kernels)
   void (*fn)(StreamArgs);
   if (f32) fn = resid ? stream_kernel<K, true, true> : stream_kernel<K, true, false>;
   else fn = resid ? stream_kernel<K, false, true> : stream_kernel<K, false, false>;

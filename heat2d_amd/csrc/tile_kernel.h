@@ -22,5 +22,9 @@ size_t tile_lds_bytes(int TX, int RY, int K);
 bool tile_config_ok(int TX, int RY, int K);
 int tile_count(int NX, int NY, int TX, int TY);
 void launch_tile(TileArgs a, int precision, bool residual, hipStream_t s);
+// No-op launches of every tiled-kernel variant of `precision`: HIP loads a translation unit's
+// code object at its first launch (deferred loading, tens to hundreds of microseconds), which
+// must not land inside a timed run.
+void warm_tile_kernels(int precision, hipStream_t s);
 
 }  // namespace h2d

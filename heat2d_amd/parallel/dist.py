@@ -33,6 +33,7 @@ class DistContext:
     local_rank: int = 0
     initialized_here: bool = False
     nccl_group: Optional[object] = None
+    distinct_devices: bool = False  # one GPU per rank (set by the caller that maps ranks to devices)
 
     @property
     def is_multi(self) -> bool:
@@ -56,6 +57,25 @@ class DistContext:
         t = torch.tensor([float(x)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
+
+    def allreduce_min(self, x: float) -> float:
+        if not self.is_multi:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return float(t.item())
+
+    def device_barrier(self, device: int) -> bool:
+        """Align the ranks at the device level: an RCCL all-reduce of one word on each rank's own
+        GPU, then a device synchronize.  Ranks leave it within a few microseconds of each other
+        (a gloo barrier's exit skew is tens of microseconds).  Only with one GPU per rank (RCCL
+        refuses two ranks on one device); returns False when not applicable."""
+        if not self.is_multi or not getattr(self, "distinct_devices", False):
+            return False
+        t = torch.ones(1, device=torch.device("cuda", device))
+        dist.all_reduce(t, group=self.get_nccl_group())
+        torch.cuda.synchronize(device)
+        return True
 
     def broadcast_bytes(self, data: Optional[bytes], src: int = 0) -> bytes:
         if not self.is_multi:

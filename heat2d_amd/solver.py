@@ -157,15 +157,21 @@ class Solver:
 
     def _make_engine(self, transport: int, ranks):
         cfg, n = self.cfg, native()
+        from .utils.benchmark import PIPELINE_OPTIONS
+
         kw = dict(tblock=cfg.tblock, rows_per_wave=cfg.rows_per_wave, small_grid_lds=cfg.small_grid,
-                  tiled={"auto": -1, "on": 1, "off": 0}[cfg.tiled])
+                  tiled={"auto": -1, "on": 1, "off": 0}[cfg.tiled], overlap=cfg.overlap)
+        if cfg.pipeline not in PIPELINE_OPTIONS:
+            raise ValueError(f"unknown pipeline {cfg.pipeline!r}")
+        kw.update(PIPELINE_OPTIONS[cfg.pipeline])
         kw.update(getattr(self, "engine_kw", {}))
         return n.Engine(
             cfg.nx, cfg.ny, gridx=self.gridx, gridy=self.gridy, periodic_x=self.model.periodic_x,
             periodic_y=self.model.periodic_y, boundary=self.model.boundary_id(), precision=self.model.precision_id(),
             init=self.model.init_id(), cx=self.model.cx, cy=self.model.cy, convergence=cfg.convergence,
             interval=cfg.interval, sensitivity=cfg.sensitivity, device=self.device, ranks=ranks,
-            transport=transport, overlap=cfg.overlap, naive=cfg.naive, **kw)
+            transport=transport, naive=cfg.naive, halo_timeout_s=cfg.halo_timeout_s,
+            sync_mode=cfg.sync_mode, **kw)
 
     # ---- data access -------------------------------------------------------------------
     def tiles(self):
@@ -285,4 +291,6 @@ class Solver:
         self.ctx.barrier()
 
     def close(self) -> None:
+        """Release the engine (device buffers, streams, RCCL communicator) now."""
+        self.exchanger = None
         self.engine = None

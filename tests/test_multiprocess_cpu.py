@@ -88,30 +88,49 @@ def test_gloo_heat2dn_strips_text(native, tmp_path):
     assert (tmp_path / "final.dat").read_text() == format_text(ref, "heat2dn")
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
-def test_bench_contract_cpu_rehearsal(tmp_path, n):
-    """bench.py under torch.distributed.run: one JSON line from rank 0, whole-job value."""
-    import json
-
+def _bench(n, args, cwd):
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env["HEAT2D_NO_BUILD"] = "1"
-    args = ["--gpus", str(n), "--steps", "6", "--warmup", "2", "--side", "48", "--device", "cpu"]
     if n == 1:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
                "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), *args]
-    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, cwd=str(cwd), env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
-    d = json.loads(lines[0])
+    import json
+
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_bench_contract_cpu_rehearsal(tmp_path, n):
+    """bench.py under torch.distributed.run: one JSON line from rank 0, whole-job value, the
+    default strong-scaling config (one grid split over N), label from the actual run, the
+    correctness gate and the in-job single-rank reference (speedup/efficiency, verified)."""
+    d = _bench(n, ["--gpus", str(n), "--steps", "6", "--warmup", "2", "--side", "48", "--device", "cpu"], tmp_path)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-              "vs_baseline", "dtype", "data", "config"):
+              "vs_baseline", "dtype", "data", "config", "speedup", "efficiency"):
         assert k in d
-    assert d["n_gpus"] == n and d["steps"] == 6 and d["scaling"] == "weak"
-    gx, gy = d["config"]["grid"]
-    assert d["config"]["grid_per_gpu"] == [48, 48]
-    assert gx * gy == 48 * 48 * n
-    assert abs(d["value"] - gx * gy * 6 / d["elapsed_s"]) / d["value"] < 1e-9
+    assert d["n_gpus"] == n and d["steps"] == 6 and d["scaling"] == "strong"
+    assert d["config"]["grid"] == [48, 48] and d["config"]["grid_per_gpu"] == [48 // n, 48]
+    assert d["metric"] == "cell-updates/sec (whole node) + speedup/efficiency, 48^2 grid 6 steps"
+    assert d["config"]["parallelism"] == ("single" if n == 1 else f"rows{n}")
+    assert abs(d["value"] - 48 * 48 * 6 / d["elapsed_s"]) / d["value"] < 1e-9
+    assert abs(d["efficiency"] - d["speedup"] / n) < 1e-12
+    if n > 1:
+        assert d["verified"] is True  # every rank's tile == the single-rank grid, bit for bit
+        assert d["gate"][0]["ok"] and d["config"]["transport"] == "torch"
+    else:
+        assert d["speedup"] == 1.0 and d["gate"] is None
+
+
+def test_bench_weak_and_blocks_cpu_rehearsal(tmp_path):
+    d = _bench(4, ["--gpus", "4", "--steps", "5", "--warmup", "1", "--config", "weak-4096", "--side", "40",
+                   "--layout", "blocks", "--device", "cpu"], tmp_path)
+    assert d["scaling"] == "weak" and d["config"]["grid"] == [80, 80] and d["config"]["grid_per_gpu"] == [40, 40]
+    assert d["config"]["parallelism"] == "blocks2x2" and d["verified"] is None
+    assert abs(d["speedup"] - 4 * d["efficiency"]) < 1e-12

@@ -48,10 +48,13 @@ def test_gpu_ranks_host_transport_match_oracle(native, gpu, tmp_path, n, gx, gy,
 
 
 def test_gpu_bench_two_ranks_host_transport(tmp_path):
+    """Two ranks on the one GPU: the gate, the strong-scaling default and the in-job
+    single-GPU reference with bit-exact verification of the timed run."""
     out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "40", "--warmup", "8", "--side",
-                        "1024", "--transport", "host", "--prewarm-s", "0"], str(tmp_path))
+                        "1024", "--prewarm-s", "0"], str(tmp_path))
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 40 and d["config"]["grid"] == [2048, 1024]
-    assert d["value"] > 0 and d["config"]["transport"] == "host"
+    assert d["n_gpus"] == 2 and d["steps"] == 40 and d["config"]["grid"] == [1024, 1024]
+    assert d["value"] > 0 and d["config"]["transport"] == "host" and d["scaling"] == "strong"
+    assert d["gate"][0]["ok"] and d["verified"] is True and d["speedup"] > 0
