@@ -58,7 +58,7 @@ def main() -> int:
     ap.add_argument("--boundary", choices=("fixed", "ghost-zero"), default="fixed")
     ap.add_argument("--tblock", type=int, default=8)
     ap.add_argument("--rows-per-wave", type=int, default=0)
-    ap.add_argument("--transport", choices=("auto", "rccl", "torch", "host"), default="auto")
+    ap.add_argument("--transport", choices=("auto", "ipc", "rccl", "torch", "host"), default="auto")
     ap.add_argument("--pipeline", choices=("auto", "signal", "concurrent", "boundary-first", "serial"), default="auto")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-gate", action="store_true", help="skip the pre-timing correctness gate (N > 1)")

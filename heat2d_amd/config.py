@@ -42,7 +42,7 @@ class Config:
     report: str = "grad"
     text_style: str = "grad"
     device: str = "auto"  # auto | gpu | cpu
-    transport: str = "auto"  # auto | local | rccl | torch | host
+    transport: str = "auto"  # auto | local | ipc | rccl | torch | host
     tblock: int = 8
     rows_per_wave: int = 0
     overlap: bool = True
@@ -123,9 +123,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="initial/final dumps: text (.dat), raw binary (*_binary.dat), both or none")
     p.add_argument("--outdir", default=".", help="directory for output files")
     p.add_argument("--device", choices=("auto", "gpu", "cpu"), default="auto")
-    p.add_argument("--transport", choices=("auto", "local", "rccl", "torch", "host"), default="auto",
-                   help="halo transport: in-process tiles, native RCCL, torch.distributed p2p (nccl backend "
-                        "on GPUs), or host (gloo p2p with host staging; also allows several ranks per GPU)")
+    p.add_argument("--transport", choices=("auto", "local", "ipc", "rccl", "torch", "host"), default="auto",
+                   help="halo transport: in-process tiles, direct IPC peer stores (1-D row strips), native RCCL, "
+                        "torch.distributed p2p (nccl backend on GPUs), or host (gloo p2p with host staging; also "
+                        "allows several ranks per GPU)")
     p.add_argument("--tblock", type=int, default=8, help="time steps fused per kernel (halo depth)")
     p.add_argument("--rows-per-wave", type=int, default=0, help="rows per wave work unit (0 = auto)")
     p.add_argument("--no-overlap", action="store_true", help="do not overlap halo exchange with interior compute")

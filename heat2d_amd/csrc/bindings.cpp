@@ -192,6 +192,7 @@ PYBIND11_MODULE(_heat2d, m) {
   m.attr("TRANSPORT_LOCAL") = (int)kTransportLocal;
   m.attr("TRANSPORT_RCCL") = (int)kTransportRccl;
   m.attr("TRANSPORT_EXTERNAL") = (int)kTransportExternal;
+  m.attr("TRANSPORT_IPC") = (int)kTransportIpc;
   m.attr("TEXT_GRAD") = (int)kTextGrad;
   m.attr("TEXT_HEAT2DN") = (int)kTextHeat2dn;
   m.attr("WAVE_COLS") = kWaveCols;
@@ -328,6 +329,17 @@ PYBIND11_MODULE(_heat2d, m) {
         e.init_rccl(s, n, r);
       })
       .def("rccl_ready", &Engine::rccl_ready)
+      .def("ipc_handle", [](Engine& e) { return py::bytes(e.ipc_handle()); })
+      .def("ipc_open",
+           [](Engine& e, const std::vector<py::bytes>& hs) {
+             std::vector<std::string> v;
+             for (auto& h : hs) v.push_back(std::string(h));
+             py::gil_scoped_release nogil;
+             e.ipc_open(v);
+           })
+      .def("ipc_prime", &Engine::ipc_prime, py::call_guard<py::gil_scoped_release>())
+      .def("ipc_primed", &Engine::ipc_primed)
+      .def("direct", &Engine::direct)
       .def("run",
            [](Engine& e, int64_t steps) {
              RunStats s;

@@ -112,6 +112,12 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     throw std::invalid_argument("local transport needs every tile in this process");
   if (transport_ == kTransportRccl && ranks.size() != 1) throw std::invalid_argument("RCCL transport: one tile per process");
   if (transport_ == kTransportRccl && !on_gpu()) throw std::invalid_argument("RCCL transport needs a GPU");
+  if (transport_ == kTransportIpc) {
+    if (ranks.size() != 1 || !on_gpu()) throw std::invalid_argument("IPC transport: one tile per process, on a GPU");
+    if (o.gridy != 1 || o.periodic_y)
+      throw std::invalid_argument("IPC transport: 1-D row strips only (gridy == 1, not periodic in y)");
+  }
+  direct_ = transport_ == kTransportIpc && has_exchange_;
 
   contig_ = transport_ == kTransportRccl && o.contiguous_halo != 0 && o.gridy == 1 && !o.periodic_y;
   if (on_gpu()) {
@@ -193,10 +199,16 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       tiles_[t].pcap = 256;
       tiles_[t].partials = dmalloc<double>(256);
     }
+    // Bounded device waits report through these (direct and signalled pipelines).
+    d_sig_timeout_ = dmalloc<unsigned int>(1);
+    H2D_HIP_CHECK(hipMemset(d_sig_timeout_, 0, sizeof(unsigned int)));
+    H2D_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_timeout_), sizeof(unsigned int), hipHostMallocMapped));
+    *h_timeout_ = 0u;
+    H2D_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_timeout_dev_), h_timeout_, 0));
     // Signalled pipeline (default with an exchange): one launch per chunk, halo-dependent
     // units first, the exchange gated mid-kernel on their completion counter.
     sig_mode_ = 0;
-    if (has_exchange_ && opt_.overlap && !opt_.naive && opt_.signal_exchange != 0) {
+    if (has_exchange_ && opt_.overlap && !opt_.naive && opt_.signal_exchange != 0 && !direct_) {
       sig_mode_ = opt_.signal_exchange < 0 ? 2 : opt_.signal_exchange;
       if (sig_mode_ == 1) {
         int ok = 0;
@@ -214,11 +226,6 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
         sig_counter_ = dmalloc<unsigned long long>(8);
       }
       H2D_HIP_CHECK(hipMemset(sig_counter_, 0, sizeof(unsigned long long)));
-      d_sig_timeout_ = dmalloc<unsigned int>(1);
-      H2D_HIP_CHECK(hipMemset(d_sig_timeout_, 0, sizeof(unsigned int)));
-      H2D_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_timeout_), sizeof(unsigned int), hipHostMallocMapped));
-      *h_timeout_ = 0u;
-      H2D_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_timeout_dev_), h_timeout_, 0));
       dev_wait_ = opt_.device_halo_wait != 0;
       if (dev_wait_) {
         halo_counter_ = dmalloc<unsigned long long>(8);
@@ -228,7 +235,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     // Overlap mode: run the halo-dependent boundary units CONCURRENTLY with the interior
     // (second stream) when they are few — e.g. 1-D row decompositions — otherwise first.
     concurrent_ = false;
-    if (has_exchange_ && opt_.overlap && opt_.concurrent != 0 && sig_mode_ == 0) {
+    if (has_exchange_ && opt_.overlap && opt_.concurrent != 0 && sig_mode_ == 0 && !direct_) {
       if (opt_.concurrent > 0) {
         concurrent_ = true;
       } else {
@@ -260,7 +267,13 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     }
     for (int t = 0; t < (int)tiles_.size(); ++t)
       for (int K = 1; K <= G_; ++K)
-        if (stream_k_supported(K)) units(t, K);
+        if (stream_k_supported(K)) {
+          const UnitLists& L = units(t, K);
+          if (direct_ && L.sig_rows <= 0)
+            throw std::invalid_argument("IPC transport: the tile is too short for full-size halo units (" +
+                                        std::to_string(tiles_[t].g.xcell) + " rows, halo depth " +
+                                        std::to_string(G_) + ")");
+        }
     // LDS-tiled path: one tile owning the whole grid (any periodic halo is its own wrap).
     const bool self_only = tiles_.size() == 1 && transport_ == kTransportLocal;
     if (self_only && !opt_.naive && opt_.tiled != 0) {
@@ -316,6 +329,10 @@ Engine::~Engine() {
     hipFree(kv.second.d_boundary);
     hipFree(kv.second.d_bfirst);
   }
+  for (size_t r = 0; r < ipc_blocks_.size(); ++r)
+    if (ipc_opened_[r]) hipIpcCloseMemHandle(ipc_blocks_[r]);
+  hipFree(ipc_block_);
+  hipFree(d_ipc_blocks_);
   hipFree(sig_counter_);
   hipFree(d_sig_timeout_);
   if (h_timeout_) hipHostFree(h_timeout_);
@@ -386,7 +403,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   // auto headroom (4096^2 row-periodic RCCL self-exchange, us/step: 14.3 -> 10.4-10.9 with
   // 16 in the concurrent pipeline; 14.3 -> 12.6 with 32 in the boundary-first one)
   const int64_t reserve = opt_.reserve_waves >= 0 ? opt_.reserve_waves : ((concurrent_ || sig_mode_ > 0) ? 16 : 32);
-  if (has_exchange_ && opt_.overlap && !P.boundary.empty() && (concurrent_ || sig_mode_ > 0 || reserve > 0)) {
+  if (!direct_ && has_exchange_ && opt_.overlap && !P.boundary.empty() && (concurrent_ || sig_mode_ > 0 || reserve > 0)) {
     // interior units leave room for what runs beside them: the boundary units (concurrent
     // and signalled pipelines) and the exchange kernels
     const int64_t nb = (concurrent_ || sig_mode_ > 0) ? (int64_t)P.boundary.size() : 0;
@@ -403,9 +420,17 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   // for most of the launch and shrank the interior).
   L.sig_rows = 0;
   const bool ns_only = !peer[kW] && !peer[kE] && !peer[kNW] && !peer[kNE] && !peer[kSW] && !peer[kSE];
-  if (sig_mode_ > 0 && opt_.overlap && has_exchange_ && ns_only && (peer[kN] || peer[kS]) && opt_.signal_plan != 0) {
-    const int64_t reserve_sig = opt_.reserve_waves >= 0 ? opt_.reserve_waves : 16;
-    UnitPlan Q = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
+  // The direct (IPC) pipeline uses the same plan; nothing runs beside its launches, so it
+  // keeps no wave slots in reserve.
+  if (((sig_mode_ > 0 && opt_.overlap && opt_.signal_plan != 0) || direct_) && has_exchange_ && ns_only &&
+      (peer[kN] || peer[kS])) {
+    const int64_t reserve_sig = direct_ ? 0 : opt_.reserve_waves >= 0 ? opt_.reserve_waves : 16;
+    // First the capacity-fitted plan; if its strip-end units are too short to be halo units,
+    // retry with units of at least 2*max(K, G) rows (fewer, taller units).
+    for (int attempt = 0; attempt < 2 && L.sig_rows == 0; ++attempt) {
+    const int Hq = attempt == 0 ? opt_.rows_per_wave : std::max(opt_.rows_per_wave, 2 * std::max(K, G_));
+    if (attempt == 1 && Hq == opt_.rows_per_wave) break;
+    UnitPlan Q = plan_units(g, K, Hq, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                             opt_.edge_weight, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, hb);
     std::map<int, std::pair<int, int>> ends;  // strip -> (top unit, bottom unit) indices
     for (int i = 0; i < (int)Q.interior.size(); ++i) {
@@ -420,6 +445,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
       const int ti = kv.second.first, bi = kv.second.second;
       if (ti == bi) {
         if (peer[kN] || peer[kS]) role[ti] = 3;
+        if (direct_) ok = false;  // one unit would need both halos and push both ways
         continue;
       }
       if (peer[kN]) role[ti] = 1;
@@ -445,6 +471,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
       P.boundary = sg;
       L.sig_rows = G_;  // released rows cover the deepest exchange that can follow
     }
+    }
   }
   std::vector<Unit>& in = P.interior;
   std::vector<Unit>& bd = P.boundary;
@@ -453,6 +480,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   if (all.size() > (size_t)(1 << 30)) throw std::runtime_error("too many work units");
   L.H = 0;
   for (const Unit& u : in) L.H = std::max(L.H, u.h);
+  for (const Unit& u : bd) ++L.n_dir[(u.flags & kUnitReverse) ? 1 : 0];
   L.n_all = (int)all.size();
   L.n_interior = (int)in.size();
   L.n_boundary = (int)bd.size();
@@ -518,17 +546,42 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     a.units = L.d_bfirst;
     a.nunits = L.n_all;
     a.prot = L.n_interior;
-    a.signal = sig_counter_;
     a.nsignal = L.n_boundary;
     a.sig_rows = L.sig_rows;
-    sig_target_ += (unsigned long long)L.n_boundary;
-    if (dev_wait_) {
-      a.halo_ready = halo_counter_;
-      a.halo_need = halo_seq_;
-      // ~1-2 us per system-scope poll (s_sleep 2 between polls)
-      a.halo_polls = std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6));
-      a.timed_out = d_sig_timeout_;
-      a.timed_out_host = h_timeout_dev_;
+    a.halo_polls = std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6));  // ~1-2 us per poll
+    a.timed_out = d_sig_timeout_;
+    a.timed_out_host = h_timeout_dev_;
+    if (direct_) {
+      // Direct pipeline: chunk c reads the ghost rows the neighbours pushed during their chunk
+      // c-1 (receive buffers of parity c), and pushes its own first G rows into the
+      // neighbours' buffers of parity c+1 (their chunk c+1 reads them).
+      const TileGeom& g = tl.g;
+      const int p = (int)(ipc_chunk_ & 1), q = p ^ 1;
+      const int pn = dec_.neighbor(tl.rank, kN), ps = dec_.neighbor(tl.rank, kS);
+      const int64_t rowb = g.pitch * (int64_t)sizeof(float);
+      if (pn >= 0) {
+        a.wait[0] = reinterpret_cast<const unsigned long long*>(ipc_block_ + ipc_lay_.flag_n);
+        a.need[0] = ipc_need_[0];
+        a.hsrc[0] = reinterpret_cast<const float*>(ipc_block_ + ipc_lay_.recv_n[p]);  // rows -G..-1
+        a.push[0] = reinterpret_cast<float*>(ipc_blocks_[pn] + ipc_lay_.recv_s[q]);     // N's rows xcell.. = my 0..
+        a.sig[0] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pn] + ipc_lay_.flag_s);
+      }
+      if (ps >= 0) {
+        a.wait[1] = reinterpret_cast<const unsigned long long*>(ipc_block_ + ipc_lay_.flag_s);
+        a.need[1] = ipc_need_[1];
+        // ghost row i (xcell <= i < xcell+G) is receive row i - xcell
+        a.hsrc[1] = reinterpret_cast<const float*>(ipc_block_ + ipc_lay_.recv_s[p] - (g.G + g.xcell) * rowb);
+        // my row i (xcell-G <= i < xcell) is S's ghost row i - xcell, its receive row i - xcell + G
+        a.push[1] = reinterpret_cast<float*>(ipc_blocks_[ps] + ipc_lay_.recv_n[q] - (g.xcell - g.G) * rowb);
+        a.sig[1] = reinterpret_cast<unsigned long long*>(ipc_blocks_[ps] + ipc_lay_.flag_n);
+      }
+    } else {
+      a.sig[0] = a.sig[1] = sig_counter_;
+      sig_target_ += (unsigned long long)L.n_boundary;
+      if (dev_wait_) {
+        a.wait[0] = a.wait[1] = halo_counter_;
+        a.need[0] = a.need[1] = halo_seq_;
+      }
     }
   }
   launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
@@ -731,6 +784,7 @@ void Engine::exchange_landed() {
 
 std::string Engine::pipeline() const {
   if (!has_exchange_) return "none";
+  if (direct_) return "direct";
   if (sig_mode_ > 0) return "signal";
   if (concurrent_) return opt_.comm_boundary != 0 ? "concurrent" : "concurrent3";
   return opt_.overlap ? "boundary-first" : "serial";
@@ -812,6 +866,7 @@ void Engine::wait_event(hipEvent_t ev) {
 }
 
 double Engine::finish_residual() {
+  if (direct_) return ipc_allreduce_residual();
   if (on_gpu() && rccl_comm_) {
     // Local sum over tiles (one tile under RCCL) -> all-reduce across ranks on the compute stream.
     H2D_NCCL_CHECK(ncclAllReduce(d_resid_, d_resid_ + tiles_.size(), 1, ncclDouble, ncclSum, (ncclComm_t)rccl_comm_,
@@ -826,6 +881,8 @@ double Engine::finish_residual() {
 
 void Engine::rollback() {
   for (Tile& t : tiles_) t.cur = 1 - t.cur;
+  // the neighbours' receive buffers hold rows of the undone chunk: a new prime is needed
+  if (direct_) ipc_primed_ = false;
 }
 
 RunStats Engine::run(int64_t steps) {
@@ -848,7 +905,8 @@ void Engine::poll_abort() {
   broken_ = true;
   broken_why_ = std::string("signalled halo pipeline timed out: ") +
                 ((to & 1) ? "the exchange gate (boundary units never completed) " : "") +
-                ((to & 2) ? "the device-side halo wait (the exchange never landed)" : "");
+                ((to & 2) ? "the device-side halo wait (the exchange never landed) " : "") +
+                ((to & 4) ? "the residual all-reduce (a rank never contributed)" : "");
   hipStreamSynchronize(comm_);
   hipStreamSynchronize(compute_);
   throw std::runtime_error(broken_why_);
@@ -860,6 +918,9 @@ RunStats Engine::run_impl(int64_t steps) {
     throw std::runtime_error("external transport: drive the loop from the caller");
   if (transport_ == kTransportRccl && has_exchange_ && !rccl_comm_)
     throw std::runtime_error("RCCL transport selected but init_rccl() was not called");
+  if (direct_ && !ipc_primed_)
+    throw std::runtime_error("IPC transport: ipc_open() + ipc_prime() needed before a run (and after upload / a "
+                             "converged run)");
   RunStats st;
   const auto w0 = std::chrono::steady_clock::now();
   const int64_t target = steps_done_ + steps;
@@ -955,7 +1016,40 @@ RunStats Engine::run_impl(int64_t steps) {
     st.chunks = 1;
   } else {
     st.path = opt_.naive ? "naive" : "stream";
-    if (has_exchange_ && sig_mode_ > 0) {
+    if (direct_) {
+      // Direct pipeline (IPC, 1-D row strips): ONE launch per chunk on ONE stream.  Its halo
+      // units (top / bottom unit of every column strip) first wait in the kernel until the
+      // neighbours' pushes for this chunk have landed (flags in my uncached block), read their
+      // ghost rows from my receive buffers, and as soon as their first G output rows are
+      // final they store them into the neighbours' receive buffers over xGMI, release them at
+      // system scope and bump the neighbours' flags.  No comm stream, no RCCL kernel, no
+      // host round trip: the exchange of chunk c+1 rides inside chunk c.
+      bool check = false;
+      int k = next_chunk(steps_done_, target, &check);
+      while (k > 0) {
+        trace_begin("chunk", compute_);
+        launch_chunk_tile(0, k, check, 3);
+        trace_end("chunk", compute_);
+        const UnitLists& L = units(0, k);
+        ipc_need_[0] += (unsigned long long)L.n_dir[0];
+        ipc_need_[1] += (unsigned long long)L.n_dir[1];
+        ++ipc_chunk_;
+        tiles_[0].cur = 1 - tiles_[0].cur;
+        ++st.chunks;
+        ++st.exchanges;
+        poll_abort();
+        if (check) {
+          st.residual = finish_residual();
+          if (st.residual < opt_.sensitivity) {
+            rollback();
+            st.converged = true;
+            break;
+          }
+        }
+        steps_done_ += k;
+        k = next_chunk(steps_done_, target, &check);
+      }
+    } else if (has_exchange_ && sig_mode_ > 0) {
       // Signalled pipeline (per chunk c), two streams:
       //   compute: ONE launch of every unit of chunk c, halo-dependent units first (they are
       //            dispatched first and are short); each of them waits in the kernel until
@@ -1339,6 +1433,7 @@ std::vector<float> Engine::download(int t) const {
 void Engine::upload(int t, const float* owned) {
   check_tile(t);
   Tile& T = tiles_[t];
+  if (direct_) ipc_primed_ = false;  // the neighbours must receive the new boundary rows
   if (on_gpu()) {
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
     H2D_HIP_CHECK(hipMemcpy2D(T.buf[T.cur] + T.g.idx(0, 0), T.g.pitch * sizeof(float), owned, T.g.ycell * sizeof(float),
@@ -1376,6 +1471,119 @@ void Engine::init_rccl(const std::string& id, int nranks, int rank) {
   rccl_rank_ = rank;
   rccl_nranks_ = nranks;
   transport_ = kTransportRccl;
+}
+
+// ---- IPC direct transport ----------------------------------------------------------------
+
+void Engine::ipc_layout() {
+  // One uncached (MTYPE UC) device block per rank: every access goes to memory, so stores a
+  // peer GPU makes over xGMI are seen by plain loads here without any cache maintenance, and
+  // polls of the flags see the peers' atomics.  Flags and counters on lines of their own.
+  const TileGeom& g = tiles_.at(0).g;
+  const size_t rb = (size_t)g.G * (size_t)g.pitch * sizeof(float);  // G full storage rows
+  const size_t rs = (rb + 4095) & ~size_t(4095);
+  IpcLayout L;
+  size_t off = 4096;  // flags / residual slots live in the first 4 KiB
+  for (int p = 0; p < 2; ++p) {
+    L.recv_n[p] = off;
+    off += rs;
+  }
+  for (int p = 0; p < 2; ++p) {
+    L.recv_s[p] = off;
+    off += rs;
+  }
+  L.bytes = off;
+  static_assert(512 + 2 * kIpcMaxRanks * sizeof(double) <= 4096, "IPC residual slots overflow the header");
+  ipc_lay_ = L;
+}
+
+std::string Engine::ipc_handle() {
+  if (transport_ != kTransportIpc) throw std::logic_error("ipc_handle: engine transport is not IPC");
+  if (!ipc_block_) {
+    ipc_layout();
+    H2D_HIP_CHECK(hipSetDevice(opt_.device));
+    H2D_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&ipc_block_), ipc_lay_.bytes, hipDeviceMallocUncached));
+    H2D_HIP_CHECK(hipMemset(ipc_block_, 0, ipc_lay_.bytes));
+    H2D_HIP_CHECK(hipDeviceSynchronize());
+  }
+  hipIpcMemHandle_t h;
+  H2D_HIP_CHECK(hipIpcGetMemHandle(&h, ipc_block_));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void Engine::ipc_open(const std::vector<std::string>& handles) {
+  if (!ipc_block_) throw std::logic_error("ipc_open: call ipc_handle() first");
+  const int me = tiles_.at(0).rank, nr = dec_.nranks();
+  if ((int)handles.size() != nr) throw std::invalid_argument("ipc_open: one handle per rank expected");
+  if (nr > kIpcMaxRanks) throw std::invalid_argument("ipc_open: too many ranks");
+  H2D_HIP_CHECK(hipSetDevice(opt_.device));
+  ipc_blocks_.assign(nr, nullptr);
+  ipc_opened_.assign(nr, false);
+  for (int r = 0; r < nr; ++r) {
+    if (r == me) {
+      ipc_blocks_[r] = ipc_block_;
+      continue;
+    }
+    if (handles[r].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("ipc_open: bad handle");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[r].data(), sizeof(h));
+    void* p = nullptr;
+    H2D_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    ipc_blocks_[r] = static_cast<char*>(p);
+    ipc_opened_[r] = true;
+    // the mapping must work before any kernel dereferences it (a fault here is an error, not a
+    // GPU memory fault inside the stencil)
+    unsigned long long probe = 0;
+    H2D_HIP_CHECK(hipMemcpy(&probe, ipc_blocks_[r] + ipc_lay_.flag_n, sizeof(probe), hipMemcpyDeviceToHost));
+  }
+  d_ipc_blocks_ = dmalloc<char*>((size_t)nr);
+  H2D_HIP_CHECK(hipMemcpy(d_ipc_blocks_, ipc_blocks_.data(), nr * sizeof(char*), hipMemcpyHostToDevice));
+  ipc_primed_ = false;
+}
+
+void Engine::ipc_prime() {
+  // Collective (the caller brackets it with barriers: no kernel of any rank is running):
+  // zero my flags and counters, and write my boundary rows into the neighbours' receive
+  // buffers of parity 0 (what their chunk 0 reads) — the initial halo.
+  if (ipc_blocks_.empty()) throw std::logic_error("ipc_prime: call ipc_open() first");
+  H2D_HIP_CHECK(hipSetDevice(opt_.device));
+  H2D_HIP_CHECK(hipDeviceSynchronize());
+  H2D_HIP_CHECK(hipMemset(ipc_block_, 0, 4096));
+  const Tile& T = tiles_.at(0);
+  const TileGeom& g = T.g;
+  const size_t rb = (size_t)g.G * (size_t)g.pitch * sizeof(float);
+  const int pn = dec_.neighbor(T.rank, kN), ps = dec_.neighbor(T.rank, kS);
+  const char* cur = reinterpret_cast<const char*>(T.buf[T.cur]);
+  const size_t row = (size_t)g.pitch * sizeof(float);
+  if (pn >= 0)  // my rows [0, G) -> N's receive buffer for its south ghost rows
+    H2D_HIP_CHECK(hipMemcpy(ipc_blocks_[pn] + ipc_lay_.recv_s[0], cur + (size_t)g.G * row, rb, hipMemcpyDeviceToDevice));
+  if (ps >= 0)  // my rows [xcell - G, xcell) -> S's receive buffer for its north ghost rows
+    H2D_HIP_CHECK(hipMemcpy(ipc_blocks_[ps] + ipc_lay_.recv_n[0], cur + (size_t)g.xcell * row, rb,
+                            hipMemcpyDeviceToDevice));
+  H2D_HIP_CHECK(hipDeviceSynchronize());
+  ipc_chunk_ = 0;
+  ipc_need_[0] = ipc_need_[1] = 0;
+  ipc_resid_epoch_ = 0;
+  ipc_primed_ = true;
+}
+
+double Engine::ipc_allreduce_residual() {
+  // Device all-reduce of the scalar residual over the IPC blocks: every rank stores its local
+  // sum into slot [parity][me] of every block and bumps each block's counter; each rank then
+  // waits for all contributions and sums the slots in rank order (deterministic, identical on
+  // every rank).  Parity-alternating slots: a rank reaching all-reduce e has seen everyone's
+  // contribution to e-1, so nobody still reads the slots of e-2 it overwrites.
+  ++ipc_resid_epoch_;
+  const int nr = (int)ipc_blocks_.size();
+  launch_ipc_allreduce(d_resid_, d_resid_ + tiles_.size(), d_ipc_blocks_, tiles_[0].rank, nr,
+                       (int)(ipc_resid_epoch_ & 1), (unsigned long long)nr * ipc_resid_epoch_, ipc_lay_.resid_count,
+                       ipc_lay_.resid_slots, kIpcMaxRanks,
+                       std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6)), d_sig_timeout_,
+                       h_timeout_dev_, compute_);
+  H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_ + tiles_.size(), sizeof(double), hipMemcpyDeviceToHost, compute_));
+  H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+  poll_abort();
+  return h_resid_[0];
 }
 
 }  // namespace h2d

@@ -38,6 +38,8 @@ enum Transport : int {
   kTransportLocal = 1,     // all tiles in this process
   kTransportRccl = 2,      // one tile per process, RCCL p2p
   kTransportExternal = 3,  // caller drives pack / unpack
+  kTransportIpc = 4,       // one tile per process, 1-D row strips: halo units store their rows
+                           // straight into the neighbour's receive buffer (IPC-mapped over xGMI)
 };
 
 struct EngineOptions {
@@ -158,6 +160,16 @@ class Engine {
   void init_rccl(const std::string& id, int nranks, int rank);
   bool rccl_ready() const { return rccl_comm_ != nullptr; }
 
+  // IPC direct transport (kTransportIpc).  Bootstrap, collectively: every rank calls
+  // ipc_handle(), the handles are all-gathered (index = rank), every rank calls ipc_open(all),
+  // then barrier -> ipc_prime() -> barrier.  A prime is needed again after upload() or a
+  // converged (rolled-back) run: ipc_primed() says so.
+  std::string ipc_handle();
+  void ipc_open(const std::vector<std::string>& handles);
+  void ipc_prime();
+  bool ipc_primed() const { return ipc_primed_; }
+  bool direct() const { return direct_; }
+
   // Native time loop (transports local / rccl / none).
   RunStats run(int64_t steps);
 
@@ -198,6 +210,7 @@ class Engine {
     Unit* d_bfirst = nullptr;  // boundary units, then interior units (signalled pipeline)
     int sig_rows = 0;          // > 0: boundary units are full-size and signal after this many rows
     int n_all = 0, n_interior = 0, n_boundary = 0;
+    int n_dir[2] = {0, 0};     // halo units facing north (top) / south (bottom, kUnitReverse)
   };
 
   const UnitLists& units(int t, int K);
@@ -265,6 +278,24 @@ class Engine {
   unsigned long long halo_seq_ = 0;            // exchanges enqueued (cumulative, host)
   void exchange_landed();                   // comm stream: publish halo_seq_ (or record evHalo)
   void gate_exchange();                     // comm stream: wait until sig_counter_ >= sig_target_
+  // ---- IPC direct transport ----
+  bool direct_ = false;
+  struct IpcLayout {
+    size_t flag_n = 0, flag_s = 128, resid_count = 256, resid_slots = 512;  // byte offsets
+    size_t recv_n[2] = {0, 0}, recv_s[2] = {0, 0};
+    size_t bytes = 0;
+  } ipc_lay_;
+  static constexpr int kIpcMaxRanks = 64;
+  char* ipc_block_ = nullptr;               // my uncached block: flags, residual slots, receive buffers
+  std::vector<char*> ipc_blocks_;           // every rank's block (mine included), mapped
+  std::vector<bool> ipc_opened_;            // entries from hipIpcOpenMemHandle (closed in the dtor)
+  char** d_ipc_blocks_ = nullptr;           // device copy of ipc_blocks_
+  bool ipc_primed_ = false;
+  unsigned long long ipc_chunk_ = 0;        // chunks since the prime (receive-buffer parity)
+  unsigned long long ipc_need_[2] = {0, 0};  // halo pushes expected from north / south
+  unsigned long long ipc_resid_epoch_ = 0;  // residual all-reduces since the prime
+  void ipc_layout();
+  double ipc_allreduce_residual();
   void* rccl_comm_ = nullptr;       // ncclComm_t
   int rccl_rank_ = 0, rccl_nranks_ = 1;
 };

@@ -84,18 +84,25 @@ struct StreamArgs {
   // Residual partial of unit w goes to slot (w + prot) mod nunits (a boundary-first list keeps
   // the interior-then-boundary summation order of the split launches).
   int prot = 0;
-  // Signalled halo pipeline: units [0, nsignal) release their stores at system scope and add
-  // 1 to *signal when done, so the comm stream can start the exchange mid-kernel.
+  // Halo units [0, nsignal) of the signalled / direct pipelines.  Direction d of a unit: 0 = a
+  // top unit (its ghost rows are the north halo), 1 = a bottom unit (kUnitReverse, south halo).
+  //   wait[d]/need[d]: before reading ghost rows, poll *wait[d] until it reaches need[d]
+  //                    (bounded: after halo_polls polls give up and report a timeout);
+  //   hsrc[d]:         read the ghost rows from here instead of src (storage-equivalent base:
+  //                    ghost row i lives at hsrc[d] + (G + i) * pitch + PL);
+  //   push[d]:         also store the first sig_rows output rows here (row-0-equivalent base:
+  //                    tile row i lives at push[d] + i * pitch + PL) — the neighbour's receive
+  //                    buffer, mapped over xGMI by IPC;
+  //   sig[d]:          once those rows are stored, release them at system scope and add 1 here.
+  // sig_rows > 0: signal as soon as the first sig_rows output rows (streaming order) are stored,
+  // then carry on (kUnitSigEnd: at the unit's end).
   int nsignal = 0;
-  unsigned long long* signal = nullptr;
-  // > 0: a signalling unit signals as soon as its first sig_rows output rows (in streaming
-  // order) are stored, then carries on with the rest of its rows (kUnitSigEnd: at its end)
   int sig_rows = 0;
-  // Device-side halo wait: units [0, nsignal) first poll *halo_ready until it reaches
-  // halo_need (the exchange that fills their ghost rows has landed); after halo_polls polls
-  // they give up and set bit 2 of *timed_out.
-  const unsigned long long* halo_ready = nullptr;
-  unsigned long long halo_need = 0;
+  unsigned long long* sig[2] = {nullptr, nullptr};
+  const unsigned long long* wait[2] = {nullptr, nullptr};
+  unsigned long long need[2] = {0, 0};
+  const float* hsrc[2] = {nullptr, nullptr};
+  float* push[2] = {nullptr, nullptr};
   long long halo_polls = 0;
   unsigned int* timed_out = nullptr;
   unsigned int* timed_out_host = nullptr;  // host-mapped mirror of *timed_out (polled by the host per chunk)
@@ -119,6 +126,11 @@ void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s);
 // `target`; after `max_polls` it gives up and sets *timed_out (the caller reports it).
 void launch_wait_counter(const unsigned long long* counter, unsigned long long target, unsigned int* timed_out,
                          unsigned int* timed_out_host, long long max_polls, hipStream_t s);
+// Direct (IPC) transport: scalar sum over ranks through every rank's mapped block (see
+// Engine::ipc_allreduce_residual); bounded wait, timeout bit 4.
+void launch_ipc_allreduce(const double* local, double* out, char* const* d_blocks, int me, int nranks, int parity,
+                          unsigned long long target, size_t count_off, size_t slot_off, int max_ranks,
+                          long long max_polls, unsigned int* timed_out, unsigned int* timed_out_host, hipStream_t s);
 // *counter = value with a system-scope release, once every earlier command on `s` is done.
 void launch_set_counter(unsigned long long* counter, unsigned long long value, hipStream_t s);
 // Residual of a whole tile (Σ (a-b)² over owned cells) — used by tests/ops.

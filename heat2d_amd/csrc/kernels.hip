@@ -84,6 +84,45 @@ __global__ __launch_bounds__(64) void wait_counter_kernel(const unsigned long lo
   report_timeout(timed_out, timed_out_host, 1u);
 }
 
+// Scalar all-reduce over the IPC-mapped blocks of every rank (direct transport), one lane:
+// publish my value into slot [parity][me] of every block (system-scope stores to the peers'
+// uncached memory), release, bump every block's counter, wait (bounded) until mine shows all
+// contributions of this epoch, then sum the slots in rank order — the same order on every
+// rank, so every rank gets the same bits.
+__global__ __launch_bounds__(64) void ipc_allreduce_kernel(const double* local, double* out, char* const* blocks,
+                                                           int me, int nr, int parity, unsigned long long target,
+                                                           unsigned long long count_off, unsigned long long slot_off,
+                                                           int max_ranks, long long max_polls, unsigned int* timed_out,
+                                                           unsigned int* timed_out_host) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long v = __double_as_longlong(*local);
+  for (int r = 0; r < nr; ++r) {
+    unsigned long long* slot = reinterpret_cast<unsigned long long*>(blocks[r] + slot_off) + parity * max_ranks + me;
+    __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int r = 0; r < nr; ++r)
+    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(blocks[r] + count_off), 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long* cnt = reinterpret_cast<const unsigned long long*>(blocks[me] + count_off);
+  long long i = 0;
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+    if (++i > max_polls) {
+      report_timeout(timed_out, timed_out_host, 4u);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const unsigned long long* slots = reinterpret_cast<const unsigned long long*>(blocks[me] + slot_off) + parity * max_ranks;
+  double sum = 0.0;
+  for (int r = 0; r < nr; ++r)
+    sum += __longlong_as_double(__hip_atomic_load(slots + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  *out = sum;
+}
+
 __global__ __launch_bounds__(64) void set_counter_kernel(unsigned long long* counter, unsigned long long value) {
   if (threadIdx.x == 0) __hip_atomic_store(counter, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -477,6 +516,15 @@ void launch_wait_counter(const unsigned long long* counter, unsigned long long t
                          unsigned int* timed_out_host, long long max_polls, hipStream_t s) {
   hipLaunchKernelGGL(wait_counter_kernel, dim3(1), dim3(64), 0, s, counter, target, timed_out, timed_out_host,
                      max_polls);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_ipc_allreduce(const double* local, double* out, char* const* d_blocks, int me, int nranks, int parity,
+                          unsigned long long target, size_t count_off, size_t slot_off, int max_ranks,
+                          long long max_polls, unsigned int* timed_out, unsigned int* timed_out_host, hipStream_t s) {
+  hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(1), dim3(64), 0, s, local, out, d_blocks, me, nranks, parity, target,
+                     (unsigned long long)count_off, (unsigned long long)slot_off, max_ranks, max_polls, timed_out,
+                     timed_out_host);
   H2D_HIP_CHECK(hipGetLastError());
 }
 

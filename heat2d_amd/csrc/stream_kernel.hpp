@@ -98,6 +98,9 @@ struct LaneCtx {
   bool m0, m1, m2, m3;  // per-column mask: fixed -> hold (global edge), ghost-zero -> zero (outside)
   float* sout;     // real output pointer (lanes in the output range), or a dummy slot
   int64_t spitch;  // row pitch of sout (0 for the dummy slot)
+  float* pout;     // halo push: copy of output rows [0, prows) (neighbour's receive buffer) or a dummy
+  int64_t ppitch;
+  int prows;       // 0: this unit pushes nothing (wave-uniform)
   bool st0, st1, st2, st3;  // element is an owned output cell (residual accounting)
 };
 
@@ -164,6 +167,7 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
     if (t == K) {
       const int64_t orow = ir - 2 * K;
       *reinterpret_cast<float4*>(c.sout + orow * c.spitch) = o;
+      if (orow < c.prows) *reinterpret_cast<float4*>(c.pout + orow * c.ppitch) = o;  // uniform branch
       if constexpr (RESID) {
         racc += c.st0 ? sq_diff(o.x, mid.x) : 0.0;
         racc += c.st1 ? sq_diff(o.y, mid.y) : 0.0;
@@ -176,13 +180,16 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
 }
 
 // Prologue row IR (compile-time): levels t <= IR/2 are primed.
+// Stream rows [0, K) are the unit's outer cone rows: for a halo unit, the ghost rows, read from
+// hrowp (the halo receive buffer of the direct pipeline; == rowp otherwise).
 template <int K, bool F32, int EDGE, bool FIXED, bool RESID, int IR>
-__device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4* __restrict__ rowp, int64_t pitch4,
-                                         const LaneCtx& c, const Coef& k, double& racc) {
+__device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4* __restrict__ rowp,
+                                         const float4* __restrict__ hrowp, int64_t pitch4, const LaneCtx& c,
+                                         const Coef& k, double& racc) {
   if constexpr (IR < 2 * K) {
-    const float4 v = rowp[(int64_t)IR * pitch4];
+    const float4 v = (IR < K ? hrowp : rowp)[(int64_t)IR * pitch4];
     process_row<K, F32, EDGE, FIXED, RESID, IR & 1, IR / 2>(S, v, IR, c, k, racc);
-    prologue<K, F32, EDGE, FIXED, RESID, IR + 1>(S, rowp, pitch4, c, k, racc);
+    prologue<K, F32, EDGE, FIXED, RESID, IR + 1>(S, rowp, hrowp, pitch4, c, k, racc);
   }
 }
 
@@ -200,9 +207,9 @@ __device__ __forceinline__ void unit_signal(unsigned long long* sig, int lane) {
 // sig_at > 0: signal (once) before processing stream row sig_at (a multiple of 4 past 2K),
 // i.e. once every output row < sig_at - 2K is stored.
 template <int K, bool F32, int EDGE, bool FIXED, bool RESID>
-__device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, int64_t pitch4, int n, const LaneCtx& c,
-                                         const Coef& k, double& racc, int sig_at, unsigned long long* sig,
-                                         int lane) {
+__device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const float4* __restrict__ hrowp,
+                                         int64_t pitch4, int n, const LaneCtx& c, const Coef& k, double& racc,
+                                         int sig_at, unsigned long long* sig, int lane) {
   float4 S[K][2];
 #pragma unroll
   for (int t = 0; t < K; ++t) {
@@ -213,7 +220,7 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, int64_
   float4 pf[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(2 * K + d, n - 1) * pitch4];
-  prologue<K, F32, EDGE, FIXED, RESID, 0>(S, rowp, pitch4, c, k, racc);
+  prologue<K, F32, EDGE, FIXED, RESID, 0>(S, rowp, hrowp, pitch4, c, k, racc);
 
   int ir0 = 2 * K;  // even: slot parity of sub-step d is d & 1
 #define H2D_STEADY(D)                                                        \
@@ -254,10 +261,11 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 template <int K, bool F32, bool RESID, int EDGE>
-__device__ __forceinline__ void run_edge(const float4* rowp, int64_t pitch4, int n, const LaneCtx& c, const Coef& k,
-                                         double& racc, bool fixed, int sig_at, unsigned long long* sig, int lane) {
-  if (fixed) run_unit<K, F32, EDGE, true, RESID>(rowp, pitch4, n, c, k, racc, sig_at, sig, lane);
-  else run_unit<K, F32, EDGE, false, RESID>(rowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+__device__ __forceinline__ void run_edge(const float4* rowp, const float4* hrowp, int64_t pitch4, int n,
+                                         const LaneCtx& c, const Coef& k, double& racc, bool fixed, int sig_at,
+                                         unsigned long long* sig, int lane) {
+  if (fixed) run_unit<K, F32, EDGE, true, RESID>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+  else run_unit<K, F32, EDGE, false, RESID>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
 }
 
 template <int K, bool F32, bool RESID>
@@ -266,13 +274,16 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const int w = (int)blockIdx.x * 4 + wv;
   if (w >= a.nunits) return;
   const int lane = (int)(threadIdx.x & 63);
-  if (a.halo_ready != nullptr && w < a.nsignal) {
-    // halo-dependent unit: wait until the exchange that fills its ghost rows has landed
-    // (a gate that already timed out in this engine stops every later wait: fail fast)
+  const Unit u = a.units[w];
+  const bool halo_unit = w < a.nsignal;
+  const int dir = (u.flags & kUnitReverse) ? 1 : 0;  // 0: north halo (top unit), 1: south (bottom unit)
+  if (halo_unit && a.wait[dir] != nullptr) {
+    // wait until the exchange that fills this unit's ghost rows has landed (a wait that already
+    // timed out in this engine stops every later wait: fail fast)
     if (lane == 0 && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
       long long i = 0;
       // relaxed polls (an acquire per poll is 2-3x slower per hop), ONE acquire after the match
-      while (__hip_atomic_load(a.halo_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.halo_need) {
+      while (__hip_atomic_load(a.wait[dir], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.need[dir]) {
         if (++i > a.halo_polls) {
           report_timeout(a.timed_out, a.timed_out_host, 2u);
           break;
@@ -282,7 +293,6 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
-  const Unit u = a.units[w];
   const int64_t x0 = u.x0;
   const int h = u.h;
   const int64_t cb = (int64_t)u.cb + 4 * lane;
@@ -314,22 +324,29 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   c.st1 = in_out && cb + 1 < a.ycell;
   c.st2 = in_out && cb + 2 < a.ycell;
   c.st3 = in_out && cb + 3 < a.ycell;
+  const bool pushes = halo_unit && a.push[dir] != nullptr;
+  c.prows = pushes ? a.sig_rows : 0;
+  c.pout = (pushes && in_out) ? a.push[dir] + xout * a.pitch + a.PL + cb : a.dummy + 4 * lane;
+  c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
 
-  const float4* rowp = reinterpret_cast<const float4*>(a.src + (a.G + xin) * a.pitch + a.PL + cb);
+  const int64_t soff = (a.G + xin) * a.pitch + a.PL + cb;
+  const float4* rowp = reinterpret_cast<const float4*>(a.src + soff);
+  const float4* hrowp = (halo_unit && a.hsrc[dir] != nullptr) ? reinterpret_cast<const float4*>(a.hsrc[dir] + soff)
+                                                              : rowp;
   const int64_t pitch4 = rev ? -(a.pitch >> 2) : (a.pitch >> 2);
   const int n = h + 2 * K;
   Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
   double racc = 0.0;
   // signalling units: mid-unit signal point (or the end); others never signal
-  const bool sig_unit = a.signal != nullptr && w < a.nsignal;
-  const int sig_at = !sig_unit ? -1
+  unsigned long long* sig = halo_unit ? a.sig[dir] : nullptr;
+  const int sig_at = sig == nullptr ? -1
                      : ((u.flags & kUnitSigEnd) != 0 || a.sig_rows <= 0) ? (1 << 30)
                                                                           : 2 * K + ((a.sig_rows + 3) & ~3);
   switch (u.flags & 3) {
-    case 0: run_unit<K, F32, 0, false, RESID>(rowp, pitch4, n, c, k, racc, sig_at, a.signal, lane); break;
-    case 1: run_edge<K, F32, RESID, 1>(rowp, pitch4, n, c, k, racc, fixed, sig_at, a.signal, lane); break;
-    case 2: run_edge<K, F32, RESID, 2>(rowp, pitch4, n, c, k, racc, fixed, sig_at, a.signal, lane); break;
-    default: run_edge<K, F32, RESID, 3>(rowp, pitch4, n, c, k, racc, fixed, sig_at, a.signal, lane); break;
+    case 0: run_unit<K, F32, 0, false, RESID>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane); break;
+    case 1: run_edge<K, F32, RESID, 1>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+    case 2: run_edge<K, F32, RESID, 2>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+    default: run_edge<K, F32, RESID, 3>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
   }
   if constexpr (RESID) {
     racc = wave_sum(racc);

@@ -85,6 +85,13 @@ class DistContext:
         dist.broadcast_object_list(obj, src=src)
         return obj[0]
 
+    def all_gather_bytes(self, data: bytes) -> list:
+        if not self.is_multi:
+            return [data]
+        out = [None] * self.world
+        dist.all_gather_object(out, data)
+        return out
+
     def gather_objects(self, obj, dst: int = 0):
         if not self.is_multi:
             return [obj]

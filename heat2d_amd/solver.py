@@ -109,7 +109,13 @@ class Solver:
                                           self.model.periodic_y)
         ranks = list(range(self.nranks)) if world == 1 else [self.ctx.rank]
 
-        if world == 1:
+        if self.on_gpu and cfg.transport == "ipc":
+            # direct peer stores into IPC-mapped receive buffers (1-D row strips); also valid for
+            # ranks sharing one GPU and for a single rank that is its own (periodic) neighbour
+            transport = n.TRANSPORT_IPC
+            if world == 1:
+                ranks = [0]
+        elif world == 1:
             transport = n.TRANSPORT_LOCAL
         elif self.on_gpu and cfg.transport in ("auto", "rccl"):
             transport = n.TRANSPORT_RCCL
@@ -127,7 +133,10 @@ class Solver:
         if cfg.tune and self.on_gpu and world == 1 and self.nranks == 1:
             self.tuned = autotune(cfg, self.model, self.device)
             self.engine_kw = dict(self.tuned["engine_kw"])
-        self.engine = self._make_engine(transport, ranks)
+        if transport == n.TRANSPORT_IPC:
+            self.engine = self._init_ipc(ranks)
+        else:
+            self.engine = self._make_engine(transport, ranks)
         self.exchanger = None
         if transport == n.TRANSPORT_RCCL and self.engine.has_exchange():
             ok = 1
@@ -154,6 +163,36 @@ class Solver:
                 self.engine.upload(t, full[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]])
             self.engine.set_steps_done(cfg.start_step)
         self.reporter = Reporter(cfg.report, enabled=(self.ctx.rank == 0 and not cfg.quiet))
+
+    def _init_ipc(self, ranks):
+        """Engine with the direct IPC transport: all-gather every rank's block handle, map them,
+        prime the initial halo.  Collective and failure-safe: if any rank fails (engine
+        constraints, IPC mapping), every rank raises the same error (no rank is left waiting
+        in a collective)."""
+        n, ctx = native(), self.ctx
+        eng, err = None, ""
+        try:
+            eng = self._make_engine(n.TRANSPORT_IPC, ranks)
+            h = eng.ipc_handle() if eng.has_exchange() else b""
+        except Exception as e:  # noqa: BLE001 - reported collectively below
+            err, h = f"{type(e).__name__}: {e}", b""
+        if ctx.allreduce_min(0 if err else 1) < 1:
+            raise RuntimeError(f"IPC transport unavailable on some rank ({err or 'another rank failed'})")
+        if eng.has_exchange():
+            hs = ctx.all_gather_bytes(h)
+            try:
+                eng.ipc_open(hs)
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+            if ctx.allreduce_min(0 if err else 1) < 1:
+                raise RuntimeError(f"IPC mapping failed on some rank ({err or 'another rank failed'})")
+            self._ipc_prime(eng)
+        return eng
+
+    def _ipc_prime(self, eng) -> None:
+        self.ctx.barrier()  # no rank has a kernel in flight
+        eng.ipc_prime()
+        self.ctx.barrier()  # every receive buffer holds its initial halo
 
     def _make_engine(self, transport: int, ranks):
         cfg, n = self.cfg, native()
@@ -232,6 +271,8 @@ class Solver:
         """Advance `steps` steps with whichever loop the transport needs (no barriers/timing)."""
         if self.transport == native().TRANSPORT_EXTERNAL and self.engine.has_exchange():
             return self._python_loop(steps)
+        if self.transport == native().TRANSPORT_IPC and self.engine.direct() and not self.engine.ipc_primed():
+            self._ipc_prime(self.engine)  # after a resume upload or a converged (rolled-back) run
         return self.engine.run(steps)
 
     def run(self, steps: Optional[int] = None) -> RunResult:

@@ -112,10 +112,15 @@ def candidates(transport: str, pipeline: str, world: int, on_gpu: bool, distinct
         return [("local", pipeline)]
     if not on_gpu:
         return [("torch", "serial")]
-    if not distinct_devices:  # several ranks per GPU: RCCL refuses them, gloo host staging works
+    rows = layout == "rows"
+    if not distinct_devices:  # several ranks per GPU: RCCL refuses them; IPC and gloo host staging work
+        if transport in ("auto", "ipc") and rows:
+            return [("ipc", "auto"), ("host", "serial")]
         return [("host", "serial")]
     chain: List[Tuple[str, str]] = []
     if transport == "auto":
+        # 1-D row strips: direct peer stores over xGMI first (no RCCL kernel, no comm stream)
+        chain += [("ipc", "auto")] if rows else []
         chain += [("rccl", pipeline), ("rccl", "boundary-first"), ("rccl", "serial"), ("torch", "serial")]
     else:
         chain += [(transport, pipeline)]

@@ -48,7 +48,10 @@ def test_tile_bytes_matches_engine_geometry(native):
 def test_candidate_chains():
     assert B.candidates("auto", "auto", 1, True, True, "rows") == [("local", "auto")]
     assert B.candidates("auto", "auto", 4, False, False, "rows") == [("torch", "serial")]
-    assert B.candidates("auto", "auto", 2, True, False, "rows") == [("host", "serial")]
+    assert B.candidates("auto", "auto", 2, True, False, "rows") == [("ipc", "auto"), ("host", "serial")]
+    assert B.candidates("auto", "auto", 2, True, False, "blocks") == [("host", "serial")]
     ch = B.candidates("auto", "auto", 8, True, True, "rows")
-    assert ch[0] == ("rccl", "auto") and ch[-1] == ("torch", "serial") and ("rccl", "serial") in ch
+    assert ch[0] == ("ipc", "auto") and ch[1] == ("rccl", "auto") and ch[-1] == ("torch", "serial")
+    assert ("rccl", "serial") in ch
+    assert B.candidates("auto", "auto", 8, True, True, "blocks")[0] == ("rccl", "auto")
     assert len(ch) == len(set(ch))

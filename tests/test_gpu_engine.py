@@ -265,3 +265,54 @@ def test_tiled_auto_selection(native, gpu):
     assert not native.Engine(4096, 4096, device=gpu).tiled()
     assert not native.Engine(640, 512, gridx=2, device=gpu).tiled()  # several tiles
     assert not native.Engine(640, 512, device=gpu, tiled=0).tiled()
+
+
+# ---- direct IPC transport (halo units push rows into the neighbour's receive buffers) -----
+def _ipc_engine(native, **kw):
+    eng = native.Engine(ranks=[0], transport=native.TRANSPORT_IPC, halo_timeout_s=5.0, **kw)
+    eng.ipc_open([eng.ipc_handle()])  # one rank: its own block (it is its own periodic neighbour)
+    eng.ipc_prime()
+    return eng
+
+
+@pytest.mark.parametrize("nx,ny", [(96, 300), (300, 701), (257, 4096), (64, 40)])
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("tblock", [8, 5, 16])
+def test_ipc_direct_self_exchange_row_periodic(native, gpu, nx, ny, boundary, tblock):
+    """Row-periodic single rank over the direct pipeline: every halo goes through the push /
+    flag / receive-buffer protocol (its own block), with balanced, ragged and K-changing chunks."""
+    steps = 3 * tblock + 11
+    eng = _ipc_engine(native, nx=nx, ny=ny, periodic_x=True, boundary=boundary, tblock=tblock, device=gpu,
+                      poison=True)
+    assert eng.pipeline() == "direct" and eng.direct()
+    st = eng.run(steps)
+    assert st["steps_done"] == steps and st["exchanges"] > 0
+    ref = oracle(native, nx, ny, steps, boundary, per=(True, False))["grid"]
+    assert np.array_equal(eng.download(0), ref)
+    # a second run continues the push/flag sequence (no re-prime), odd length
+    eng.run(7)
+    ref = oracle(native, nx, ny, steps + 7, boundary, per=(True, False))["grid"]
+    assert np.array_equal(eng.download(0), ref)
+
+
+def test_ipc_direct_convergence_and_reprime(native, gpu):
+    nx, ny = 96, 300
+    kw = dict(convergence=True, interval=10, sensitivity=1e12)
+    ref = oracle(native, nx, ny, 5000, 1, per=(True, False), **kw)
+    assert ref["converged"] and ref["steps_done"] == 219
+    eng = _ipc_engine(native, nx=nx, ny=ny, periodic_x=True, boundary=1, device=gpu, **kw)
+    st = eng.run(5000)
+    assert st["converged"] and st["steps_done"] == ref["steps_done"]
+    assert np.array_equal(eng.download(0), ref["grid"])
+    assert not eng.ipc_primed()  # the rollback invalidated the pushed halos
+    with pytest.raises(RuntimeError):
+        eng.run(5)
+    eng.ipc_prime()
+    eng.run(5)
+
+
+def test_ipc_direct_rejects_unsupported(native, gpu):
+    with pytest.raises(Exception):
+        native.Engine(96, 300, gridx=1, gridy=2, ranks=[0], transport=native.TRANSPORT_IPC, device=gpu)
+    with pytest.raises(Exception):  # tile too short for full-size halo units
+        native.Engine(12, 300, periodic_x=True, ranks=[0], transport=native.TRANSPORT_IPC, device=gpu)

@@ -47,11 +47,40 @@ def test_gpu_ranks_host_transport_match_oracle(native, gpu, tmp_path, n, gx, gy,
     assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
 
 
+@pytest.mark.parametrize("n,boundary,conv", [(2, "fixed", 0), (3, "ghost-zero", 0), (4, "fixed", 1)])
+def test_gpu_ranks_ipc_direct_match_oracle(native, gpu, tmp_path, n, boundary, conv):
+    """Ranks sharing the GPU through real IPC handles: direct halo pushes between processes,
+    the device all-reduce of the convergence residual, uneven row split."""
+    nx, ny, steps = 67 * n + 1, 517, 61
+    args = ["-m", "heat2d_amd", "--device", "gpu", "--transport", "ipc", "--nx", str(nx), "--ny", str(ny),
+            "--steps", str(steps), "--gridx", str(n), "--gridy", "1", "--boundary", boundary, "--output", "binary",
+            "--outdir", str(tmp_path)]
+    kw = {}
+    if conv:
+        args += ["--convergence", "1", "--interval", "6", "--sensitivity", "1e-30"]
+        kw = dict(convergence=True, interval=6, sensitivity=1e-30)
+    out = _torchrun(n, args, str(tmp_path))
+    assert f"Starting with {n} processes" in out
+    b = 0 if boundary == "fixed" else 1
+    ref = native.oracle_run(nx, ny, steps, boundary=b, **kw)["grid"]
+    assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
+
+
+def test_gpu_bench_two_ranks_ipc(tmp_path):
+    """The bench at N=2 on one GPU: the gate picks the direct IPC transport first."""
+    out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "40", "--warmup", "8", "--side",
+                        "1024", "--prewarm-s", "0"], str(tmp_path))
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    d = json.loads(lines[-1])
+    assert d["config"]["transport"] == "ipc" and d["config"]["pipeline"] == "direct"
+    assert d["gate"][0]["ok"] and d["verified"] is True
+
+
 def test_gpu_bench_two_ranks_host_transport(tmp_path):
     """Two ranks on the one GPU: the gate, the strong-scaling default and the in-job
     single-GPU reference with bit-exact verification of the timed run."""
     out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "40", "--warmup", "8", "--side",
-                        "1024", "--prewarm-s", "0"], str(tmp_path))
+                        "1024", "--prewarm-s", "0", "--transport", "host"], str(tmp_path))
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
