@@ -427,11 +427,15 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     const int64_t reserve_sig = direct_ ? 0 : opt_.reserve_waves >= 0 ? opt_.reserve_waves : 16;
     // First the capacity-fitted plan; if its strip-end units are too short to be halo units,
     // retry with units of at least 2*max(K, G) rows (fewer, taller units).
-    for (int attempt = 0; attempt < 2 && L.sig_rows == 0; ++attempt) {
-    const int Hq = attempt == 0 ? opt_.rows_per_wave : std::max(opt_.rows_per_wave, 2 * std::max(K, G_));
-    if (attempt == 1 && Hq == opt_.rows_per_wave) break;
+    // Attempts: the capacity-fitted plan; the same without shortening edge-strip units (their
+    // strip-end units may fall below G rows); units of at least 2*max(K, G) rows.
+    for (int attempt = 0; attempt < 3 && L.sig_rows == 0; ++attempt) {
+    const int Hq = attempt < 2 ? opt_.rows_per_wave : std::max(opt_.rows_per_wave, 2 * std::max(K, G_));
+    const double ew = attempt == 0 ? opt_.edge_weight : 1.0;
+    if (attempt == 1 && ew == opt_.edge_weight) continue;
+    if (attempt == 2 && Hq == opt_.rows_per_wave) break;
     UnitPlan Q = plan_units(g, K, Hq, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
-                            opt_.edge_weight, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, hb);
+                            ew, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, hb);
     std::map<int, std::pair<int, int>> ends;  // strip -> (top unit, bottom unit) indices
     for (int i = 0; i < (int)Q.interior.size(); ++i) {
       const Unit& u = Q.interior[i];

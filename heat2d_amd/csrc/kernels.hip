@@ -261,13 +261,20 @@ H2D_K_LIST(H2D_EXTERN2)
 #undef H2D_EXTERN2
 
 int64_t stream_wave_capacity(int K, int precision, int device) {
+  // The ref-precision stencil is VALU-bound (about 11 fp64-rate VALU ops per cell-step, one
+  // wave issuing ~88 % of cycles): a second resident wave on a SIMD only splits that SIMD's
+  // VALU, while halving every unit's height doubles the K-cone recompute share.  So one
+  // wave per SIMD (measured on MI355X, 4096^2 K=8: 7.81 vs 8.04 us/step; 512x4096 K=6: 2.17
+  // vs 3.13).  The fp32 path (3-4 VALU ops per cell) keeps the occupancy limit.
   int bpc = 1;
   const bool f32 = precision == kFp32;
-  switch (K) {
+  if (f32) {
+    switch (K) {
 #define H2D_CASE(KK) case KK: bpc = stream_blocks_per_cu<KK>(f32, false); break;
-    H2D_K_LIST(H2D_CASE)
+      H2D_K_LIST(H2D_CASE)
 #undef H2D_CASE
-    default: break;
+      default: break;
+    }
   }
   int cus = 256;
   hipDeviceProp_t p;

@@ -9,7 +9,7 @@ import time
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from heat2d_amd._native import native  # noqa: E402
 
 n = native()
