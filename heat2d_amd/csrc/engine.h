@@ -80,6 +80,12 @@ struct EngineOptions {
   // hipEventSynchronize; 1 no timing pair, spin on one untimed completion event; 2 no events,
   // hipStreamSynchronize; 3 timing pair, spin on the end event.  device_ms is wall time in 1/2.
   int sync_mode = 0;
+  // Direct (IPC) pipeline fences: release of a halo unit's push (0 system scope, 1 agent, 2
+  // none: the payload went to the peer's uncached memory and is acknowledged before the flag)
+  // and acquire after its halo wait (0 system, 1 agent, 2 none: ghost rows are read from
+  // uncached memory).  -1: the measured default.
+  int direct_release = -1;
+  int direct_acquire = -1;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
   bool poison = false;        // debug canary: NaN in every cell no valid update may read

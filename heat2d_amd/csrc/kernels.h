@@ -103,6 +103,8 @@ struct StreamArgs {
   unsigned long long need[2] = {0, 0};
   const float* hsrc[2] = {nullptr, nullptr};
   float* push[2] = {nullptr, nullptr};
+  int rel = 0;  // signal release: 0 system scope, 1 agent scope, 2 drain only (payload in uncached memory)
+  int acq = 0;  // halo-wait acquire: 0 system scope, 1 agent scope, 2 compiler ordering only
   long long halo_polls = 0;
   unsigned int* timed_out = nullptr;
   unsigned int* timed_out_host = nullptr;  // host-mapped mirror of *timed_out (polled by the host per chunk)

@@ -101,6 +101,7 @@ struct LaneCtx {
   float* pout;     // halo push: copy of output rows [0, prows) (neighbour's receive buffer) or a dummy
   int64_t ppitch;
   int prows;       // 0: this unit pushes nothing (wave-uniform)
+  int rel;         // release flavour of the unit's signal (unit_signal)
   bool st0, st1, st2, st3;  // element is an owned output cell (residual accounting)
 };
 
@@ -197,9 +198,14 @@ __device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4* __rest
 // them at system scope and count the unit.  Producer recipe of the MI355X guide: the wave's
 // stores drained, the release fence (L2 write-back), an explicit drain again (ROCm 7.2 can
 // drop the fence's own wait), then ONE lane's atomic add.
-__device__ __forceinline__ void unit_signal(unsigned long long* sig, int lane) {
+__device__ __forceinline__ void unit_signal(unsigned long long* sig, int lane, int rel) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // rel 0: system-scope release (L2 write-back: the RCCL path's payload lives in coarse-grained
+  // tile memory another agent may read); 1: agent scope; 2: none — the direct pipeline's payload
+  // was stored to the peer's UNCACHED memory, so the drained (acknowledged) stores are already
+  // at their destination and only the ordering of the flag after them matters.
+  if (rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  else if (rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -230,7 +236,7 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
     process_row<K, F32, EDGE, FIXED, RESID, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
   for (; ir0 + 4 <= n; ir0 += 4) {
-    if (ir0 == sig_at) unit_signal(sig, lane);
+    if (ir0 == sig_at) unit_signal(sig, lane, c.rel);
     H2D_STEADY(0)
     H2D_STEADY(1)
     H2D_STEADY(2)
@@ -243,7 +249,7 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
   if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
   // the loop visits every sig_at candidate below its exit value: a signal point at or past the
   // exit has not fired yet (unit shorter than its signal rows, or kUnitSigEnd)
-  if (sig_at >= ir0) unit_signal(sig, lane);
+  if (sig_at >= ir0) unit_signal(sig, lane, c.rel);
 }
 
 // A bounded wait gave up: set `bit` in the device word (fail-fast for later waits) and in its
@@ -291,7 +297,11 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
         __builtin_amdgcn_s_sleep(2);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    // acq 0: system scope; 1: agent scope (this CU's L1); 2: the ghost rows are in uncached
+    // memory and were polled for: only keep the compiler from hoisting their loads
+    if (a.acq == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    else if (a.acq == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   const int64_t x0 = u.x0;
   const int h = u.h;
@@ -326,6 +336,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   c.st3 = in_out && cb + 3 < a.ycell;
   const bool pushes = halo_unit && a.push[dir] != nullptr;
   c.prows = pushes ? a.sig_rows : 0;
+  c.rel = a.rel;
   c.pout = (pushes && in_out) ? a.push[dir] + xout * a.pitch + a.PL + cb : a.dummy + 4 * lane;
   c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
 
