@@ -153,7 +153,7 @@ const std::map<std::string, OptSetter>& engine_option_table() {
       H2D_OPT(precision), H2D_OPT(init), H2D_OPT(cx), H2D_OPT(cy), H2D_OPT(tblock), H2D_OPT(rows_per_wave),
       H2D_OPT(edge_weight), H2D_OPT(wave_capacity), H2D_OPT(boundary_rows), H2D_OPT(concurrent),
       H2D_OPT(comm_boundary), H2D_OPT(signal_exchange), H2D_OPT(device_halo_wait), H2D_OPT(comm_priority),
-      H2D_OPT(signal_plan), H2D_OPT(watchdog_s), H2D_OPT(halo_timeout_s), H2D_OPT(sync_mode), H2D_OPT(direct_release), H2D_OPT(direct_acquire), H2D_OPT(trace), H2D_OPT(poison), H2D_OPT(convergence),
+      H2D_OPT(signal_plan), H2D_OPT(watchdog_s), H2D_OPT(halo_timeout_s), H2D_OPT(sync_mode), H2D_OPT(fused_check), H2D_OPT(direct_release), H2D_OPT(direct_acquire), H2D_OPT(trace), H2D_OPT(poison), H2D_OPT(convergence),
       H2D_OPT(interval), H2D_OPT(sensitivity), H2D_OPT(device), H2D_OPT(ranks), H2D_OPT(transport),
       H2D_OPT(overlap), H2D_OPT(small_grid_lds), H2D_OPT(tiled), H2D_OPT(tile_rows), H2D_OPT(tile_width),
       H2D_OPT(tile_k), H2D_OPT(naive), H2D_OPT(comm_cus), H2D_OPT(comm_cu_layout), H2D_OPT(reserve_waves),

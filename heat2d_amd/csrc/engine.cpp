@@ -164,8 +164,19 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     H2D_HIP_CHECK(hipHostMalloc(&h_resid_, sizeof(double) * (ranks.size() + 1)));
     d_lds_steps_ = dmalloc<long long>(1);
     d_dummy_ = dmalloc<float>(4 * kWaveCols);
+    if (o.convergence && !o.naive && transport_ != kTransportExternal && o.fused_check != 0) {
+      d_stop_ = dmalloc<unsigned long long>(1);
+      H2D_HIP_CHECK(hipMemset(d_stop_, 0, sizeof(unsigned long long)));
+      H2D_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_conv_), sizeof(ConvHost), hipHostMallocMapped));
+      std::memset(h_conv_, 0, sizeof(ConvHost));
+      H2D_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_conv_dev_), h_conv_, 0));
+      H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_check_, hipEventDisableTiming));
+      d_ticket_ = dmalloc<unsigned int>(ranks.size());
+      H2D_HIP_CHECK(hipMemset(d_ticket_, 0, ranks.size() * sizeof(unsigned int)));
+    }
   }
 
+  fused_ = on_gpu() && o.convergence && !o.naive && transport_ != kTransportExternal && o.fused_check != 0;
   for (int r : ranks) {
     Tile t;
     t.rank = r;
@@ -175,6 +186,11 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       for (int b = 0; b < 2; ++b) {
         t.buf[b] = dmalloc<float>(n);
         H2D_HIP_CHECK(hipMemsetAsync(t.buf[b], 0, n * sizeof(float), compute_));
+      }
+      if (fused_) {
+        t.keep = dmalloc<float>(n);
+        H2D_HIP_CHECK(hipMemsetAsync(t.keep, 0, n * sizeof(float), compute_));
+        if (o.poison) launch_poison(t.g, t.keep, o.boundary == kFixed, o.periodic_x, o.periodic_y, compute_);
       }
       launch_init(t.g, t.buf[0], o.init, compute_);
       if (o.poison)
@@ -284,7 +300,10 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       // tiled / LDS solver / streaming: 80x64 0.90 / 1.56 / 1.60; 160x128 0.87 / 4.05 / 1.63;
       // 320x256 0.91 / - / 1.61; 640x512 1.36 / - / 1.89; 1280x1024 2.50 / - / 2.07.
       const int64_t cells = NX * NY;
-      const bool lds_whole = opt_.small_grid_lds && !has_exchange_ && lds_solver_fits(NX, NY) && opt_.convergence;
+      // (with the fused device-side check the tiled path converges without host round trips
+      // too, and is faster per step: it no longer yields to the whole-grid solver)
+      const bool lds_whole =
+          opt_.small_grid_lds && !has_exchange_ && lds_solver_fits(NX, NY) && opt_.convergence && !fused_;
       const bool want = opt_.tiled == 1 || (cells <= 600000 && !lds_whole);
       if (want && NX < (1 << 30) && NY < (1 << 30)) {
         int RY = opt_.tile_width > 0 ? opt_.tile_width : 64;
@@ -321,8 +340,14 @@ Engine::~Engine() {
     return;
   }
   hipDeviceSynchronize();
-  for (auto& t : tiles_)
+  for (auto& t : tiles_) {
     for (int b = 0; b < 2; ++b) hipFree(t.buf[b]);
+    if (t.keep) hipFree(t.keep);
+  }
+  if (d_stop_) hipFree(d_stop_);
+  if (d_ticket_) hipFree(d_ticket_);
+  if (h_conv_) hipHostFree(h_conv_);
+  if (ev_check_) hipEventDestroy(ev_check_);
   for (auto& kv : units_) {
     hipFree(kv.second.d_all);
     hipFree(kv.second.d_interior);
@@ -536,6 +561,15 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   a.per_y = opt_.periodic_y;
   a.partials = tl.partials;
   a.dummy = d_dummy_;
+  const bool whole = which == 0 || which == 3;  // the launch covers every unit of the tile
+  // A lone single-process tile sums its partials and decides in ONE small kernel behind the
+  // launch (device_decide).  (A last-wave in-kernel reduction was measured slower here: 1024
+  // waves' ticket atomics on one address serialise; the tiled kernel, with few blocks, uses it.)
+  const bool lone = fused_ && tiles_.size() == 1 && !rccl_comm_ && !direct_;
+  if (fused_) {
+    a.stop = d_stop_;
+    if (residual) a.keep = tl.keep;
+  }
   if (which == 0) {
     a.units = L.d_all;
     a.nunits = L.n_all;
@@ -595,7 +629,11 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     }
   }
   launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
-  if (residual && (which == 0 || which == 3)) reduce_tile_residual(t, K);
+  if (residual && whole && !lone) reduce_tile_residual(t, K);
+  if (residual && whole && lone) {
+    last_parts_ = tl.partials;
+    last_nparts_ = L.n_all;
+  }
 }
 
 void Engine::reduce_tile_residual(int t, int K) {
@@ -610,6 +648,15 @@ int Engine::chunk_len(int64_t done, int64_t total, int kmax, bool* check) const 
   *check = false;
   int64_t seg = total - done;  // steps up to the end of the run or the next check step
   if (seg <= 0) return 0;
+  if (opt_.convergence && fused_) {
+    // fused check: the check step ends its chunk (the launch keeps the state one step earlier)
+    const int64_t next_check = (done / opt_.interval + 1) * opt_.interval;
+    seg = std::min<int64_t>(seg, next_check - done);
+    const int64_t n = (seg + kmax - 1) / kmax;
+    const int64_t k = std::max<int64_t>(1, (seg + n - 1) / n);
+    *check = done + k == next_check;
+    return (int)k;
+  }
   if (opt_.convergence) {
     const int64_t next_check = (done / opt_.interval + 1) * opt_.interval;
     if (done + 1 == next_check) {
@@ -631,7 +678,9 @@ int Engine::next_chunk(int64_t done, int64_t total, bool* check) const {
   if (on_gpu() && !opt_.naive)
     while (k > 1 && !stream_k_supported((int)k)) --k;
   if (opt_.naive) k = 1;
-  return (int)std::max<int64_t>(1, k);
+  k = std::max<int64_t>(1, k);
+  if (fused_ && opt_.convergence) *check = (done + k) % opt_.interval == 0;  // k may have shrunk
+  return (int)k;
 }
 
 CopyDesc* Engine::local_descs(int K, int& n, int64_t& maxe) {
@@ -988,18 +1037,30 @@ RunStats Engine::run_impl(int64_t steps) {
       a.per_x = opt_.periodic_x;
       a.per_y = opt_.periodic_y;
       a.partials = T.partials;
+      if (fused_) {
+        a.stop = d_stop_;
+        if (check) {
+          a.keep = T.keep + T.g.idx(0, 0);
+          a.dec = decide_args(0, true);  // the last block sums the partials and decides
+          decided_in_launch_ = true;
+        }
+      }
       trace_begin("step", compute_);
       launch_tile(a, opt_.precision, check, compute_);
       trace_end("step", compute_);
-      if (check) launch_reduce_sum(T.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
+      if (check && !fused_) launch_reduce_sum(T.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
       T.cur = 1 - T.cur;
       ++st.chunks;
       if (check) {
-        st.residual = finish_residual();
-        if (st.residual < opt_.sensitivity) {
-          rollback();
-          st.converged = true;
-          break;
+        if (fused_) {
+          if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+        } else {
+          st.residual = finish_residual();
+          if (st.residual < opt_.sensitivity) {
+            rollback();
+            st.converged = true;
+            break;
+          }
         }
       }
       steps_done_ += k;
@@ -1049,11 +1110,15 @@ RunStats Engine::run_impl(int64_t steps) {
         ++st.exchanges;
         poll_abort();
         if (check) {
-          st.residual = finish_residual();
-          if (st.residual < opt_.sensitivity) {
-            rollback();
-            st.converged = true;
-            break;
+          if (fused_) {
+            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+          } else {
+            st.residual = finish_residual();
+            if (st.residual < opt_.sensitivity) {
+              rollback();
+              st.converged = true;
+              break;
+            }
           }
         }
         steps_done_ += k;
@@ -1095,11 +1160,15 @@ RunStats Engine::run_impl(int64_t steps) {
         if (check) {
           // nothing is in flight on the comm stream here (the exchange of chunk c completed
           // before the chunk started), so the all-reduce is the communicator's only operation
-          st.residual = finish_residual();
-          if (st.residual < opt_.sensitivity) {
-            rollback();
-            st.converged = true;
-            break;
+          if (fused_) {
+            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+          } else {
+            st.residual = finish_residual();
+            if (st.residual < opt_.sensitivity) {
+              rollback();
+              st.converged = true;
+              break;
+            }
           }
         }
         if (k_next > 0) {
@@ -1157,11 +1226,15 @@ RunStats Engine::run_impl(int64_t steps) {
         if (check) {
           H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[p], 0));
           for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
-          st.residual = finish_residual();
-          if (st.residual < opt_.sensitivity) {
-            rollback();
-            st.converged = true;
-            break;
+          if (fused_) {
+            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+          } else {
+            st.residual = finish_residual();
+            if (st.residual < opt_.sensitivity) {
+              rollback();
+              st.converged = true;
+              break;
+            }
           }
         }
         if (k_next > 0) {
@@ -1226,11 +1299,15 @@ RunStats Engine::run_impl(int64_t steps) {
         if (check) {
           H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[p], 0));
           for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
-          st.residual = finish_residual();
-          if (st.residual < opt_.sensitivity) {
-            rollback();
-            st.converged = true;
-            break;
+          if (fused_) {
+            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+          } else {
+            st.residual = finish_residual();
+            if (st.residual < opt_.sensitivity) {
+              rollback();
+              st.converged = true;
+              break;
+            }
           }
         }
         steps_done_ += k;
@@ -1283,11 +1360,15 @@ RunStats Engine::run_impl(int64_t steps) {
         ++st.chunks;
         if (check) {
           for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
-          st.residual = finish_residual();
-          if (st.residual < opt_.sensitivity) {
-            rollback();
-            st.converged = true;
-            break;
+          if (fused_) {
+            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+          } else {
+            st.residual = finish_residual();
+            if (st.residual < opt_.sensitivity) {
+              rollback();
+              st.converged = true;
+              break;
+            }
           }
         }
         steps_done_ += k;
@@ -1316,11 +1397,15 @@ RunStats Engine::run_impl(int64_t steps) {
         trace_end("step", compute_);
         ++st.chunks;
         if (check) {
-          st.residual = finish_residual();
-          if (st.residual < opt_.sensitivity) {
-            rollback();
-            st.converged = true;
-            break;
+          if (fused_) {
+            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+          } else {
+            st.residual = finish_residual();
+            if (st.residual < opt_.sensitivity) {
+              rollback();
+              st.converged = true;
+              break;
+            }
           }
         }
         steps_done_ += k;
@@ -1329,9 +1414,90 @@ RunStats Engine::run_impl(int64_t steps) {
   }
   end_of_run_wait(st, w0);
   poll_abort();
+  if (fused_) finalize_convergence(st);
   trace_collect(st);
   st.steps_done = steps_done_;
   return st;
+}
+
+// ---- device-side convergence (fused check) -----------------------------------------------
+
+DecideArgs Engine::decide_args(int t, bool decide) const {
+  DecideArgs d;
+  d.ticket = d_ticket_ + t;
+  d.total = decide ? d_resid_ + tiles_.size() : d_resid_ + t;
+  d.stop = d_stop_;
+  d.host = decide ? h_conv_dev_ : nullptr;
+  d.sens = opt_.sensitivity;
+  d.seq = chunk_seq_ + 1;  // the check this launch belongs to (check_point numbers it next)
+  return d;
+}
+
+void Engine::device_decide(unsigned long long seq) {
+  // Σ over this process's tiles, then over ranks, then the decision — all enqueued on the
+  // compute stream; nothing waits for the host.  (A lone single-process tile decides inside
+  // its residual launch: nothing to enqueue.)
+  const int nt = (int)tiles_.size();
+  double* total = d_resid_ + nt;
+  DecideArgs d = decide_args(0, true);
+  d.seq = seq;
+  if (direct_) {
+    ++ipc_resid_epoch_;
+    launch_ipc_allreduce(d_resid_, total, d_ipc_blocks_, tiles_[0].rank, (int)ipc_blocks_.size(),
+                         (int)(ipc_resid_epoch_ & 1), (unsigned long long)ipc_blocks_.size() * ipc_resid_epoch_,
+                         ipc_lay_.resid_count, ipc_lay_.resid_slots, kIpcMaxRanks,
+                         std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6)), d_sig_timeout_,
+                         h_timeout_dev_, d_stop_, &d, compute_);
+  } else if (rccl_comm_) {
+    H2D_NCCL_CHECK(ncclAllReduce(d_resid_, total, 1, ncclDouble, ncclSum, (ncclComm_t)rccl_comm_, compute_));
+    launch_decide(total, d, compute_);
+  } else if (last_parts_ != nullptr) {  // a lone tile: its units' partials straight to the decision
+    launch_reduce_decide(last_parts_, last_nparts_, d, compute_);
+    last_parts_ = nullptr;
+  } else {
+    launch_reduce_decide(d_resid_, nt, d, compute_);
+  }
+}
+
+bool Engine::check_point(int64_t steps_before, int k) {
+  // The chunk just enqueued ended on a check step: record it, enqueue the decision, and tell
+  // the caller whether the host already sees a converged check (then it stops enqueueing;
+  // launches queued after the converged one are no-ops on the device).
+  const unsigned long long seq = ++chunk_seq_;
+  checks_.push_back(CheckRec{seq, steps_before, k});
+  if (!decided_in_launch_) device_decide(seq);
+  decided_in_launch_ = false;
+  if (rccl_comm_) {
+    // Ranks must enqueue the same collectives: look only at fixed points of the check sequence,
+    // after the decision of that check has completed (the same answer on every rank).
+    if (++checks_since_sync_ < 16) return false;
+    checks_since_sync_ = 0;
+    H2D_HIP_CHECK(hipEventRecord(ev_check_, compute_));
+    wait_event(ev_check_);
+  }
+  return __atomic_load_n(&h_conv_->stop_seq, __ATOMIC_ACQUIRE) != 0ull;
+}
+
+void Engine::finalize_convergence(RunStats& st) {
+  const unsigned long long seq = __atomic_load_n(&h_conv_->stop_seq, __ATOMIC_ACQUIRE);
+  if (seq != 0ull) {
+    auto it = std::find_if(checks_.begin(), checks_.end(), [&](const CheckRec& r) { return r.seq == seq; });
+    if (it == checks_.end()) throw std::logic_error("converged check not found");
+    // the result is the state one step before the converged check (B-5): the level K-1 rows
+    // the check launch kept
+    steps_done_ = it->steps_before + it->k - 1;
+    for (Tile& t : tiles_) std::swap(t.keep, t.buf[t.cur]);
+    st.converged = true;
+    st.residual = h_conv_->residual;
+    H2D_HIP_CHECK(hipMemsetAsync(d_stop_, 0, sizeof(unsigned long long), compute_));
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    __atomic_store_n(&h_conv_->stop_seq, 0ull, __ATOMIC_RELEASE);
+    if (direct_) ipc_primed_ = false;  // the neighbours hold halos of later launches
+  } else if (!checks_.empty()) {
+    st.residual = h_conv_->last;
+  }
+  checks_.clear();
+  checks_since_sync_ = 0;
 }
 
 void Engine::end_of_run_wait(RunStats& st, std::chrono::steady_clock::time_point w0) {
@@ -1589,7 +1755,7 @@ double Engine::ipc_allreduce_residual() {
                        (int)(ipc_resid_epoch_ & 1), (unsigned long long)nr * ipc_resid_epoch_, ipc_lay_.resid_count,
                        ipc_lay_.resid_slots, kIpcMaxRanks,
                        std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6)), d_sig_timeout_,
-                       h_timeout_dev_, compute_);
+                       h_timeout_dev_, nullptr, nullptr, compute_);
   H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_ + tiles_.size(), sizeof(double), hipMemcpyDeviceToHost, compute_));
   H2D_HIP_CHECK(hipStreamSynchronize(compute_));
   poll_abort();

@@ -84,6 +84,10 @@ struct EngineOptions {
   // none: the payload went to the peer's uncached memory and is acknowledged before the flag)
   // and acquire after its halo wait (0 system, 1 agent, 2 none: ghost rows are read from
   // uncached memory).  -1: the measured default.
+  // Convergence decided on the device (checks end a chunk, the check launch keeps the state one
+  // step earlier, later launches see a stop word): no host round trip per check.  -1 auto (GPU,
+  // native loop), 0 the host-synchronised 1-step check chunk.
+  int fused_check = -1;
   int direct_release = -1;
   int direct_acquire = -1;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
@@ -201,6 +205,7 @@ class Engine {
     int rank = 0;
     TileGeom g;
     float* buf[2] = {nullptr, nullptr};  // device or host storage
+    float* keep = nullptr;               // fused convergence: state one step before the last check
     std::vector<float> host[2];          // CPU storage
     std::vector<float> scratch[2];       // CPU temporal-block scratch
     int cur = 0;
@@ -301,6 +306,28 @@ class Engine {
   unsigned long long ipc_need_[2] = {0, 0};  // halo pushes expected from north / south
   unsigned long long ipc_resid_epoch_ = 0;  // residual all-reduces since the prime
   void ipc_layout();
+  // ---- device-side convergence ----
+  bool fused_ = false;
+  unsigned long long* d_stop_ = nullptr;  // 0 running, else the sequence number of the converged check
+  ConvHost* h_conv_ = nullptr;            // host-mapped decision record
+  ConvHost* h_conv_dev_ = nullptr;
+  unsigned long long chunk_seq_ = 0;
+  struct CheckRec {
+    unsigned long long seq;
+    int64_t steps_before;
+    int k;
+  };
+  std::vector<CheckRec> checks_;
+  int checks_since_sync_ = 0;
+  hipEvent_t ev_check_ = nullptr;
+  unsigned int* d_ticket_ = nullptr;      // per tile: last-wave tickets of fused residual launches
+  bool decided_in_launch_ = false;        // the last check launch already made the decision
+  const double* last_parts_ = nullptr;    // a lone tile's residual partials awaiting the decision
+  int last_nparts_ = 0;
+  DecideArgs decide_args(int t, bool decide) const;
+  void device_decide(unsigned long long seq);
+  bool check_point(int64_t steps_before, int k);
+  void finalize_convergence(RunStats& st);
   double ipc_allreduce_residual();
   void* rccl_comm_ = nullptr;       // ncclComm_t
   int rccl_rank_ = 0, rccl_nranks_ = 1;

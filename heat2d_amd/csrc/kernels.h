@@ -65,6 +65,26 @@ UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, boo
 // Resident waves of the streaming kernel on `device` (occupancy query × CUs × 4 waves/block).
 int64_t stream_wave_capacity(int K, int precision, int device);
 
+// Host-mapped record of the device-side convergence decisions.
+struct ConvHost {
+  unsigned long long stop_seq;  // 0: running, else the sequence number of the converged check
+  double residual;              // total of the converged check
+  double last;                  // total of the latest check
+  unsigned long long checks;
+};
+// Convergence decision of check `seq` made on the device by whoever holds the total: the last
+// wave of a residual launch (fused epilogue), or a reduction kernel.  ticket != nullptr: the
+// launch's residual partials are summed and decided in-kernel by the wave whose ticket add
+// comes last (it resets the ticket for the next check).
+struct DecideArgs {
+  unsigned int* ticket = nullptr;
+  double* total = nullptr;
+  unsigned long long* stop = nullptr;
+  ConvHost* host = nullptr;
+  double sens = 0.0;
+  unsigned long long seq = 0;
+};
+
 // Arguments of the temporally-blocked streaming stencil.
 struct StreamArgs {
   const float* src;
@@ -103,6 +123,13 @@ struct StreamArgs {
   unsigned long long need[2] = {0, 0};
   const float* hsrc[2] = {nullptr, nullptr};
   float* push[2] = {nullptr, nullptr};
+  // Device-side convergence (fused check): a launch whose *stop is non-zero does nothing (its
+  // halo units only signal, so gates and flags stay in step); a residual launch also stores
+  // the level K-1 value of every output cell into `keep` (same layout as dst) — the state one
+  // step before the check, which the run returns if the check converges (B-5 semantics).
+  const unsigned long long* stop = nullptr;
+  float* keep = nullptr;
+  DecideArgs dec;  // residual launches of a single-tile run: fused sum + decision
   int rel = 0;  // signal release: 0 system scope, 1 agent scope, 2 drain only (payload in uncached memory)
   int acq = 0;  // halo-wait acquire: 0 system scope, 1 agent scope, 2 compiler ordering only
   long long halo_polls = 0;
@@ -132,7 +159,11 @@ void launch_wait_counter(const unsigned long long* counter, unsigned long long t
 // Engine::ipc_allreduce_residual); bounded wait, timeout bit 4.
 void launch_ipc_allreduce(const double* local, double* out, char* const* d_blocks, int me, int nranks, int parity,
                           unsigned long long target, size_t count_off, size_t slot_off, int max_ranks,
-                          long long max_polls, unsigned int* timed_out, unsigned int* timed_out_host, hipStream_t s);
+                          long long max_polls, unsigned int* timed_out, unsigned int* timed_out_host,
+                          const unsigned long long* stop, const DecideArgs* decide, hipStream_t s);
+void launch_decide(const double* sum, const DecideArgs& d, hipStream_t s);
+// Σ in[0..n) (fixed order) and the decision in one launch.
+void launch_reduce_decide(const double* in, int n, const DecideArgs& d, hipStream_t s);
 // *counter = value with a system-scope release, once every earlier command on `s` is done.
 void launch_set_counter(unsigned long long* counter, unsigned long long value, hipStream_t s);
 // Residual of a whole tile (Σ (a-b)² over owned cells) — used by tests/ops.

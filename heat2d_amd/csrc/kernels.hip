@@ -93,8 +93,12 @@ __global__ __launch_bounds__(64) void ipc_allreduce_kernel(const double* local, 
                                                            int me, int nr, int parity, unsigned long long target,
                                                            unsigned long long count_off, unsigned long long slot_off,
                                                            int max_ranks, long long max_polls, unsigned int* timed_out,
-                                                           unsigned int* timed_out_host) {
+                                                           unsigned int* timed_out_host,
+                                                           const unsigned long long* stop, DecideArgs d,
+                                                           int decide) {
   if (threadIdx.x != 0) return;
+  // after a converged check no rank contributes any more (each stops on its own schedule)
+  if (stop != nullptr && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;
   const unsigned long long v = __double_as_longlong(*local);
   for (int r = 0; r < nr; ++r) {
     unsigned long long* slot = reinterpret_cast<unsigned long long*>(blocks[r] + slot_off) + parity * max_ranks + me;
@@ -121,6 +125,22 @@ __global__ __launch_bounds__(64) void ipc_allreduce_kernel(const double* local, 
   for (int r = 0; r < nr; ++r)
     sum += __longlong_as_double(__hip_atomic_load(slots + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
   *out = sum;
+  if (decide) decide_total(sum, d);
+}
+
+__global__ __launch_bounds__(64) void decide_kernel(const double* sum, DecideArgs d) {
+  if (threadIdx.x == 0) decide_total(*sum, d);
+}
+
+// Deterministic sum of n partials (the same fixed order as publish_partial) + the decision.
+__global__ __launch_bounds__(64) void reduce_decide_kernel(const double* __restrict__ in, int n, DecideArgs d) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 64) s += in[i];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) {
+    *d.total = s;
+    decide_total(s, d);
+  }
 }
 
 __global__ __launch_bounds__(64) void set_counter_kernel(unsigned long long* counter, unsigned long long value) {
@@ -528,10 +548,23 @@ void launch_wait_counter(const unsigned long long* counter, unsigned long long t
 
 void launch_ipc_allreduce(const double* local, double* out, char* const* d_blocks, int me, int nranks, int parity,
                           unsigned long long target, size_t count_off, size_t slot_off, int max_ranks,
-                          long long max_polls, unsigned int* timed_out, unsigned int* timed_out_host, hipStream_t s) {
+                          long long max_polls, unsigned int* timed_out, unsigned int* timed_out_host,
+                          const unsigned long long* stop, const DecideArgs* decide, hipStream_t s) {
+  DecideArgs d;
+  if (decide) d = *decide;
   hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(1), dim3(64), 0, s, local, out, d_blocks, me, nranks, parity, target,
                      (unsigned long long)count_off, (unsigned long long)slot_off, max_ranks, max_polls, timed_out,
-                     timed_out_host);
+                     timed_out_host, stop, d, decide ? 1 : 0);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_decide(const double* sum, const DecideArgs& d, hipStream_t s) {
+  hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(64), 0, s, sum, d);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_reduce_decide(const double* in, int n, const DecideArgs& d, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_decide_kernel, dim3(1), dim3(64), 0, s, in, n, d);
   H2D_HIP_CHECK(hipGetLastError());
 }
 

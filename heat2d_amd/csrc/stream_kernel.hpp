@@ -102,6 +102,8 @@ struct LaneCtx {
   int64_t ppitch;
   int prows;       // 0: this unit pushes nothing (wave-uniform)
   int rel;         // release flavour of the unit's signal (unit_signal)
+  float* kout;     // RESID launches: level K-1 value of each output cell (rollback state) or a dummy
+  int64_t kpitch;  // row pitch of kout (0 for the dummy slot)
   bool st0, st1, st2, st3;  // element is an owned output cell (residual accounting)
 };
 
@@ -170,6 +172,7 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
       *reinterpret_cast<float4*>(c.sout + orow * c.spitch) = o;
       if (orow < c.prows) *reinterpret_cast<float4*>(c.pout + orow * c.ppitch) = o;  // uniform branch
       if constexpr (RESID) {
+        *reinterpret_cast<float4*>(c.kout + orow * c.kpitch) = mid;
         racc += c.st0 ? sq_diff(o.x, mid.x) : 0.0;
         racc += c.st1 ? sq_diff(o.y, mid.y) : 0.0;
         racc += c.st2 ? sq_diff(o.z, mid.z) : 0.0;
@@ -274,6 +277,43 @@ __device__ __forceinline__ void run_edge(const float4* rowp, const float4* hrowp
   else run_unit<K, F32, EDGE, false, RESID>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
 }
 
+// The decision of a convergence check, by the one lane that holds the total.
+__device__ __forceinline__ void decide_total(double r, const DecideArgs& d) {
+  if (*d.stop != 0ull) return;  // already stopped
+  __hip_atomic_store(&d.host->last, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&d.host->checks, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (r < d.sens) {
+    *d.stop = d.seq;
+    __hip_atomic_store(&d.host->residual, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&d.host->stop_seq, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Fused check epilogue (one wave): publish this wave's partial; with d.ticket, the wave whose
+// ticket add is the last of `nparts` sums all partials in a fixed order and decides.  The
+// partials are stored write-through (agent-scope atomic store = sc1) and drained before the
+// ticket add, the last adder acquires before reading them (MI355X guide, G16 row 1).
+__device__ __forceinline__ void publish_partial(double* partials, int slot, double v, int nparts,
+                                                const DecideArgs& d, int lane) {
+  if (lane == 0) __hip_atomic_store(partials + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (d.ticket == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int last = 0;
+  if (lane == 0) last = __hip_atomic_fetch_add(d.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        (unsigned)(nparts - 1);
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double s = 0.0;
+  for (int i = lane; i < nparts; i += 64) s += __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  s = wave_sum(s);
+  if (lane == 0) {
+    *d.total = s;
+    if (d.host != nullptr) decide_total(s, d);  // else a cross-tile / cross-rank sum decides later
+    __hip_atomic_store(d.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int K, bool F32, bool RESID>
 __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -283,6 +323,13 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const Unit u = a.units[w];
   const bool halo_unit = w < a.nsignal;
   const int dir = (u.flags & kUnitReverse) ? 1 : 0;  // 0: north halo (top unit), 1: south (bottom unit)
+  if (a.stop != nullptr && __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) {
+    // converged earlier in this run: no work, but halo units still count, so gates / flags of
+    // launches already queued on other streams and ranks stay in step
+    if (halo_unit && a.sig[dir] != nullptr && lane == 0)
+      __hip_atomic_fetch_add(a.sig[dir], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   if (halo_unit && a.wait[dir] != nullptr) {
     // wait until the exchange that fills this unit's ghost rows has landed (a wait that already
     // timed out in this engine stops every later wait: fail fast)
@@ -337,6 +384,9 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const bool pushes = halo_unit && a.push[dir] != nullptr;
   c.prows = pushes ? a.sig_rows : 0;
   c.rel = a.rel;
+  const bool keeps = a.keep != nullptr && in_out;
+  c.kout = keeps ? a.keep + (out - a.dst) : a.dummy + 4 * lane;
+  c.kpitch = keeps ? c.spitch : 0;
   c.pout = (pushes && in_out) ? a.push[dir] + xout * a.pitch + a.PL + cb : a.dummy + 4 * lane;
   c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
 
@@ -363,7 +413,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     racc = wave_sum(racc);
     int slot = w + a.prot;
     if (slot >= a.nunits) slot -= a.nunits;
-    if (lane == 0) a.partials[slot] = racc;
+    publish_partial(a.partials, slot, racc, a.nunits, a.dec, lane);
   }
 }
 

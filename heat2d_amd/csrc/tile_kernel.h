@@ -17,6 +17,9 @@ struct TileArgs {
   double cx, cy;
   int fixed, per_x, per_y;
   double* partials;  // [ntiles] residual partials (residual launches)
+  const unsigned long long* stop = nullptr;  // converged earlier: the launch does nothing
+  float* keep = nullptr;  // residual launches: level K-1 of the owned tile (rollback state)
+  DecideArgs dec;         // residual launches: fused sum + decision (last block)
 };
 size_t tile_lds_bytes(int TX, int RY, int K);
 bool tile_config_ok(int TX, int RY, int K);

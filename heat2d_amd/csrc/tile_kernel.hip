@@ -42,6 +42,7 @@ __global__ __launch_bounds__(256) void tile_lds_kernel(TileArgs a) {
   // XCD-aware tile order: block b runs on XCD b % 8; give each XCD a contiguous tile range
   int b = blockIdx.x;
   if (b >= a.ntiles) return;
+  if (a.stop != nullptr && __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;
   if (a.ntiles % 8 == 0) b = (b & 7) * (a.ntiles >> 3) + (b >> 3);
   const int bx = b / a.tiles_y, by = b - bx * a.tiles_y;
   const int x0 = bx * a.TX - K;  // global row of region row 0
@@ -138,14 +139,19 @@ __global__ __launch_bounds__(256) void tile_lds_kernel(TileArgs a) {
   const int xs = bx * a.TX, ys = by * a.TY;
   for (int e = tid; e < a.TX * a.TY; e += 256) {
     const int i = e / a.TY, j = e - i * a.TY;
-    if (xs + i < a.NX && ys + j < a.NY) a.dst[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + 4 + K + j];
+    if (xs + i < a.NX && ys + j < a.NY) {
+      a.dst[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + 4 + K + j];
+      // after the final swap `nxt` holds level K-1
+      if (RESID && a.keep != nullptr) a.keep[(int64_t)(xs + i) * a.pitch + (ys + j)] = nxt[(K + i) * W + 4 + K + j];
+    }
   }
   if constexpr (RESID) {
     __shared__ double part[4];
     racc = wave_sum(racc);
     if ((tid & 63) == 0) part[tid >> 6] = racc;
     __syncthreads();
-    if (tid == 0) a.partials[blockIdx.x] = ((part[0] + part[1]) + part[2]) + part[3];
+    if (tid < 64) publish_partial(a.partials, blockIdx.x, ((part[0] + part[1]) + part[2]) + part[3], a.ntiles, a.dec,
+                                  tid);
   }
 }
 

@@ -316,3 +316,78 @@ def test_ipc_direct_rejects_unsupported(native, gpu):
         native.Engine(96, 300, gridx=1, gridy=2, ranks=[0], transport=native.TRANSPORT_IPC, device=gpu)
     with pytest.raises(Exception):  # tile too short for full-size halo units
         native.Engine(12, 300, periodic_x=True, ranks=[0], transport=native.TRANSPORT_IPC, device=gpu)
+
+
+# ---- fused (device-side) convergence: checks end a chunk, no host round trip --------------
+CONV = dict(convergence=True, interval=9, sensitivity=1.93e13)  # ghost-zero 257x509: converges at 98 steps
+
+
+def _gather(eng, nx, ny):
+    out = np.zeros((nx, ny), np.float32)
+    for t in range(eng.num_tiles()):
+        g = eng.geom(t)
+        out[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]] = eng.download(t)
+    return out
+
+
+@pytest.mark.parametrize("gx,gy", [(1, 1), (2, 1), (1, 2)])
+@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5, 6])
+def test_fused_convergence_matches_oracle(native, gpu, gx, gy, pipeline):
+    nx, ny = 257, 509
+    ref = oracle(native, nx, ny, 3000, 1, **CONV)
+    assert ref["converged"] and ref["steps_done"] == 98
+    for fused in (-1, 0):
+        eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
+                            small_grid_lds=False, tiled=0, **PIPELINES[pipeline], **CONV)
+        st = eng.run(3000)
+        assert st["converged"] and st["steps_done"] == ref["steps_done"], (fused, st)
+        assert abs(st["residual"] - ref["residual"]) <= 1e-9 * ref["residual"]
+        assert np.array_equal(_gather(eng, nx, ny), ref["grid"]), (gx, gy, pipeline, fused)
+        # continuing re-checks at step 99 against the converged state: converged again, same state
+        st2 = eng.run(5)
+        assert st2["converged"] and st2["steps_done"] == ref["steps_done"]
+        assert np.array_equal(_gather(eng, nx, ny), ref["grid"])
+
+
+@pytest.mark.parametrize("interval", [1, 4, 8, 9, 20])
+@pytest.mark.parametrize("tblock", [8, 5])
+def test_fused_convergence_intervals(native, gpu, interval, tblock):
+    nx, ny = 257, 509
+    kw = dict(convergence=True, interval=interval, sensitivity=2.68e13)
+    ref = oracle(native, nx, ny, 3000, 1, **kw)
+    assert ref["converged"]
+    eng = native.Engine(nx, ny, boundary=1, tblock=tblock, device=gpu, small_grid_lds=False, tiled=0, poison=True,
+                        **kw)
+    st = eng.run(3000)
+    assert st["converged"] and st["steps_done"] == ref["steps_done"]
+    assert np.array_equal(eng.download(0), ref["grid"])
+
+
+def test_fused_convergence_tiled_and_split_runs(native, gpu):
+    nx, ny = 257, 509
+    ref = oracle(native, nx, ny, 3000, 1, **CONV)
+    eng = native.Engine(nx, ny, boundary=1, device=gpu, tiled=1, tile_k=8, small_grid_lds=False, **CONV)
+    st = eng.run(3000)
+    assert st["path"] == "tiled" and st["converged"] and st["steps_done"] == 98
+    assert np.array_equal(eng.download(0), ref["grid"])
+    # a run split into pieces that end between checks converges at the same step
+    eng = native.Engine(nx, ny, boundary=1, device=gpu, tiled=0, small_grid_lds=False, **CONV)
+    done = 0
+    for piece in (13, 22, 31, 3000):
+        st = eng.run(piece)
+        done = st["steps_done"]
+        if st["converged"]:
+            break
+    assert st["converged"] and done == 98 and np.array_equal(eng.download(0), ref["grid"])
+
+
+def test_fused_convergence_rccl_and_ipc_self(native, gpu):
+    nx, ny = 96, 300
+    kw = dict(convergence=True, interval=10, sensitivity=1e12)
+    ref = oracle(native, nx, ny, 5000, 1, per=(True, False), **kw)
+    eng = native.Engine(nx, ny, periodic_x=True, boundary=1, device=gpu, ranks=[0], transport=native.TRANSPORT_RCCL,
+                        **kw)
+    eng.init_rccl(native.Engine.rccl_unique_id(), 1, 0)
+    st = eng.run(5000)
+    assert st["converged"] and st["steps_done"] == ref["steps_done"] == 219
+    assert np.array_equal(eng.download(0), ref["grid"])

@@ -1,0 +1,41 @@
+"""Table-4-style measurement on one MI355X: 1000 steps of each reference grid with and without
+the convergence check every 20 steps (sensitivity 0: the check runs but never stops the run,
+as in the reference's timed runs), device-side fused check vs the host-synchronised one.
+Prints a markdown table (seconds for 1000 steps, like Report.pdf Tables 1 and 4)."""
+import os
+import sys
+import time
+
+import torch  # noqa: F401
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from heat2d_amd._native import native  # noqa: E402
+
+n = native()
+grids = [(80, 64), (160, 128), (320, 256), (640, 512), (1280, 1024), (2560, 2048), (4096, 4096)]
+steps = 1000
+
+
+def timed(**kw):
+    e = n.Engine(device=0, boundary=1, **kw)  # grad semantics (zero ghost ring), as the reference's MPI code
+    e.run(200)
+    best = 1e9
+    for _ in range(3):
+        e.synchronize()
+        t0 = time.perf_counter()
+        st = e.run(steps)
+        e.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    assert st["steps_done"] == e.steps_done()
+    return best, st["path"]
+
+
+print("| grid | no check (s) | check every 20, fused (s) | overhead | check every 20, host-synced (s) | overhead | path |")
+print("|---|---|---|---|---|---|---|")
+for nx, ny in grids:
+    t0, path = timed(nx=nx, ny=ny)
+    conv = dict(convergence=True, interval=20, sensitivity=0.0)
+    t1, _ = timed(nx=nx, ny=ny, **conv)
+    t2, _ = timed(nx=nx, ny=ny, fused_check=0, **conv)
+    print(f"| {nx}x{ny} | {t0:.3e} | {t1:.3e} | {100 * (t1 / t0 - 1):+.1f} % | {t2:.3e} | {100 * (t2 / t0 - 1):+.1f} % "
+          f"| {path} |", flush=True)
