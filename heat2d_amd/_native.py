@@ -14,35 +14,29 @@ from __future__ import annotations
 import importlib
 import os
 
-# Hardware queues per process: the engine runs the compute stream and the comm stream (halo
-# exchange gate, RCCL, completion counter) concurrently, and HIP maps streams onto at most
-# GPU_MAX_HW_QUEUES in-order hardware queues.  With 4, streams created by other engines /
-# libraries shift the round-robin map until the two share one queue, which serialises the
-# exchange behind the stencil (measured: 9.5 -> 15 us/step on the multi-rank proxy,
-# tools/gpu_probe_queues.sh).  8 gives every stream its own queue.  Read once at HIP init,
-# so it is set here, before torch (or anything) touches the GPU.
-if os.environ.get("HEAT2D_KEEP_HW_QUEUES") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
-
 import torch  # noqa: E402,F401  (must precede the native module, see above)
 
 _mod = None
 
 
 def native():
-    """Return the loaded ``_heat2d`` module (building it first if needed)."""
+    """Return the loaded ``_heat2d`` module.  The extension carries the hash of the native
+    sources it was built from; if it is missing or stale (sources edited since), it is rebuilt
+    in-tree first — or, with ``HEAT2D_NO_BUILD=1`` (GPU boxes, the driver), the import FAILS
+    rather than run a binary that does not match the sources."""
     global _mod
     if _mod is not None:
         return _mod
-    try:
-        _mod = importlib.import_module("heat2d_amd._heat2d")
-    except ImportError:
-        if os.environ.get("HEAT2D_NO_BUILD") == "1":
-            raise
-        from . import _build
+    from . import _build
 
+    want = _build.source_hash() if os.path.isdir(_build.CSRC) else None
+    have = _build.stamped_hash(_build.EXT_PATH)
+    if want is not None and have != want:
+        if os.environ.get("HEAT2D_NO_BUILD") == "1":
+            raise ImportError(f"heat2d_amd native extension is stale or missing (built from {have}, sources are "
+                              f"{want}): run `python -m heat2d_amd._build`")
         _build.build(cli=False)
-        _mod = importlib.import_module("heat2d_amd._heat2d")
+    _mod = importlib.import_module("heat2d_amd._heat2d")
     return _mod
 
 

@@ -144,7 +144,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       H2D_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
       // Optionally a high-priority comm stream (its waves win dispatch ties against the
       // stencil's).  Separate hardware queues for compute and comm come from
-      // GPU_MAX_HW_QUEUES >= 8 (heat2d_amd/_native.py), not from the priority.
+      // GPU_MAX_HW_QUEUES >= 8 (set by the bench / CLI entry points), not from the priority.
       int least = 0, greatest = 0;
       if (o.comm_priority > 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least) {
         H2D_HIP_CHECK(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, greatest));
@@ -160,6 +160,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     H2D_HIP_CHECK(hipEventCreate(&ev_t0_));
     H2D_HIP_CHECK(hipEventCreate(&ev_t1_));
     H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+    for (auto& e : ev_prog_) H2D_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     d_resid_ = dmalloc<double>(ranks.size() + 1);
     H2D_HIP_CHECK(hipHostMalloc(&h_resid_, sizeof(double) * (ranks.size() + 1)));
     d_lds_steps_ = dmalloc<long long>(1);
@@ -376,6 +377,8 @@ Engine::~Engine() {
   hipEventDestroy(ev_t0_);
   hipEventDestroy(ev_t1_);
   hipEventDestroy(ev_done_);
+  for (auto& e : ev_prog_)
+    if (e) hipEventDestroy(e);
   if (bstream_) hipStreamDestroy(bstream_);
   for (int i = 0; i < 2; ++i) {
     if (ev_i_[i]) hipEventDestroy(ev_i_[i]);
@@ -629,6 +632,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     }
   }
   launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
+  progress_tick(stream ? stream : compute_);
   if (residual && whole && !lone) reduce_tile_residual(t, K);
   if (residual && whole && lone) {
     last_parts_ = tl.partials;
@@ -893,10 +897,18 @@ double Engine::local_residual() {
   return s;
 }
 
+void Engine::progress_tick(hipStream_t s) {
+  if (!rccl_comm_ || (++launches_ % 16) != 0) return;
+  const int i = (int)((launches_ / 16) % kProgRing);
+  H2D_HIP_CHECK(hipEventRecord(ev_prog_[i], s));
+  prog_seq_[i] = launches_;
+}
+
 void Engine::wait_event(hipEvent_t ev) {
   // Failure detection: with a communicator, poll the event and RCCL's asynchronous error
-  // state instead of blocking, and abort the communicator after `watchdog_s` without
-  // completion (a dead peer would otherwise hang the rank forever).
+  // state instead of blocking, and abort the communicator after `watchdog_s` WITHOUT PROGRESS
+  // (no newer progress event completed — a dead peer would otherwise hang the rank forever;
+  // a long healthy run keeps completing launches and is never aborted).
   if (!ev) {
     H2D_HIP_CHECK(hipEventRecord(ev_done_, compute_));
     ev = ev_done_;
@@ -905,17 +917,25 @@ void Engine::wait_event(hipEvent_t ev) {
     H2D_HIP_CHECK(hipEventSynchronize(ev));
     return;
   }
-  const auto t0 = std::chrono::steady_clock::now();
+  auto t0 = std::chrono::steady_clock::now();
   for (unsigned spin = 0;; ++spin) {
     const hipError_t e = hipEventQuery(ev);
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) H2D_HIP_CHECK(e);
+    if ((spin & 63) == 0) {
+      for (int i = 0; i < kProgRing; ++i)
+        if (prog_seq_[i] > prog_seen_ && hipEventQuery(ev_prog_[i]) == hipSuccess) {
+          prog_seen_ = prog_seq_[i];
+          t0 = std::chrono::steady_clock::now();
+        }
+    }
     ncclResult_t async = ncclSuccess;
     ncclCommGetAsyncError((ncclComm_t)rccl_comm_, &async);
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (async != ncclSuccess || (opt_.watchdog_s > 0 && el > opt_.watchdog_s)) {
       const std::string why = async != ncclSuccess ? std::string("RCCL async error: ") + ncclGetErrorString(async)
-                                                   : "watchdog: no progress for " + std::to_string(el) + " s";
+                                                   : "watchdog: no progress (completed launch) for " +
+                                                         std::to_string(el) + " s";
       ncclCommAbort((ncclComm_t)rccl_comm_);
       rccl_comm_ = nullptr;
       throw std::runtime_error("[rank " + std::to_string(rccl_rank_) + "] " + why);

@@ -231,7 +231,14 @@ class Engine {
   void reduce_tile_residual(int t, int K);
   void do_exchange_async(int K);  // enqueue on comm stream
   double finish_residual();       // reduce + (rccl) all-reduce, host sync
-  void wait_event(hipEvent_t ev);  // blocking wait with RCCL error polling + watchdog
+  void wait_event(hipEvent_t ev);  // blocking wait with RCCL error polling + progress watchdog
+  // Progress events for the watchdog: every 16th launch records one (ring of 8); a wait resets
+  // its no-progress clock whenever a newer one has completed.
+  static constexpr int kProgRing = 8;
+  hipEvent_t ev_prog_[kProgRing] = {};
+  unsigned long long prog_seq_[kProgRing] = {};
+  unsigned long long launches_ = 0, prog_seen_ = 0;
+  void progress_tick(hipStream_t s);
   int chunk_len(int64_t done, int64_t total, int kmax, bool* check) const;  // convergence-aligned chunk
   RunStats run_impl(int64_t steps);
   CopyDesc* local_descs(int K, int& n, int64_t& maxe);

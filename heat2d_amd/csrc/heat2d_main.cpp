@@ -31,19 +31,30 @@ struct Preset {
   int boundary;
   double cx;
   bool convergence;
+  int64_t interval;
+  double sensitivity;
   std::string report, text;
   bool binary;
   bool strips;
 };
 
+// The preset table lives in presets.def (shared with the Python package).
 const std::map<std::string, Preset>& presets() {
-  static const std::map<std::string, Preset> p = {
-      {"heat2d", {10, 10, 100, 1, 1, kFixed, kCxDouble, false, "grad", "grad", true, false}},
-      {"heat2dn", {10, 10, 100, 1, 1, kFixed, kCxFloat, false, "heat2dn", "heat2dn", false, true}},
-      {"grad_mpi", {10, 10, 100, 2, 2, kGhostZero, kCxDouble, false, "grad", "grad", true, false}},
-      {"grad_hybrid", {10, 10, 100, 1, 1, kGhostZero, kCxDouble, true, "hybrid", "grad", true, false}},
-      {"cuda", {640, 1024, 10000, 1, 1, kFixed, kCxDouble, false, "cuda", "none", false, false}},
-  };
+  static const std::map<std::string, Preset> p = [] {
+    const int fixed = kFixed, ghost_zero = kGhostZero;
+    const double dbl = kCxDouble, flt = kCxFloat;
+    (void)fixed;
+    (void)ghost_zero;
+    (void)dbl;
+    (void)flt;
+    std::map<std::string, Preset> m;
+#define H2D_PRESET(name, nx, ny, steps, gx, gy, bnd, coeff, conv, interval, sens, report, text, binary, dec) \
+  m[#name] = Preset{nx, ny, steps, gx, gy, bnd, std::string(#coeff) == "float" ? flt : dbl, conv != 0, interval,   \
+                    sens, #report, #text, binary != 0, std::string(#dec) == "strips"};
+#include "presets.def"
+#undef H2D_PRESET
+    return m;
+  }();
   return p;
 }
 
@@ -103,11 +114,12 @@ int main(int argc, char** argv) {
   const int64_t steps = geti("steps", P.steps);
   o.gridx = (int)geti("gridx", P.gridx);
   o.gridy = (int)geti("gridy", P.gridy);
+  if (o.gridx == 0) o.gridx = 1;  // automatic: the world size, one process here
   if (o.gridx < 1 || o.gridy < 1) usage("gridx/gridy must be >= 1 in the single-process program");
   if (P.strips && !a.count("gridy")) o.gridy = 1;
   o.convergence = geti("convergence", P.convergence ? 1 : 0) != 0;
-  o.interval = geti("interval", 20);
-  o.sensitivity = getd("sensitivity", 0.1);
+  o.interval = geti("interval", P.interval);
+  o.sensitivity = getd("sensitivity", P.sensitivity);
   o.cx = getd("cx", P.cx);
   o.cy = getd("cy", P.cx);
   o.boundary = P.boundary;

@@ -23,6 +23,8 @@ preset         reference program and its semantics
 """
 from __future__ import annotations
 
+import os
+import re
 from dataclasses import dataclass, field
 from typing import Dict
 
@@ -53,15 +55,26 @@ class Preset:
         return CX_FLOAT if self.coeff == "float" else CX_DOUBLE
 
 
-PRESETS: Dict[str, Preset] = {
-    "heat2d": Preset("heat2d", 10, 10, 100, 1, 1, "fixed", "double", False, 20, 0.1, "grad", "grad", True),
-    "heat2dn": Preset("heat2dn", 10, 10, 100, 0, 1, "fixed", "float", False, 20, 0.1, "heat2dn", "heat2dn", False,
-                      decomposition="strips"),
-    "grad_mpi": Preset("grad_mpi", 10, 10, 100, 2, 2, "ghost-zero", "double", False, 20, 0.1, "grad", "grad", True),
-    "grad_hybrid": Preset("grad_hybrid", 10, 10, 100, 1, 1, "ghost-zero", "double", True, 20, 0.1, "hybrid", "grad",
-                          True),
-    "cuda": Preset("cuda", 640, 1024, 10000, 1, 1, "fixed", "double", False, 20, 0.1, "cuda", "none", False),
-}
+def _load_presets() -> Dict[str, Preset]:
+    """Parse the shared preset table ``csrc/presets.def`` (also compiled into the C++ CLI)."""
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "presets.def")
+    out: Dict[str, Preset] = {}
+    with open(path, encoding="utf-8") as f:
+        for line in f:
+            m = re.match(r"\s*H2D_PRESET\((.*)\)\s*$", line)
+            if not m:
+                continue
+            (name, nx, ny, steps, gx, gy, bnd, coeff, conv, interval, sens, report, text, binary,
+             dec) = [t.strip() for t in m.group(1).split(",")]
+            out[name] = Preset(name, int(nx), int(ny), int(steps), int(gx), int(gy), bnd.replace("_", "-"), coeff,
+                               conv != "0", int(interval), float(sens), report, text, binary != "0",
+                               decomposition=dec)
+    if not out:
+        raise RuntimeError(f"no presets parsed from {path}")
+    return out
+
+
+PRESETS: Dict[str, Preset] = _load_presets()
 
 
 @dataclass

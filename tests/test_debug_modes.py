@@ -114,3 +114,99 @@ def test_host_sanitizers(tmp_path):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0", UBSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+
+
+ENGINE_SAN_DRIVER = r"""
+#include <cstdio>
+#include <cstring>
+#include <vector>
+#include "cpu_reference.h"
+#include "decomposition.h"
+#include "engine.h"
+#include "kernels.h"
+using namespace h2d;
+static int check_engine(int64_t nx, int64_t ny, int gx, int gy, int K, int boundary, bool px, bool py, bool conv) {
+  EngineOptions o;
+  o.nx = nx; o.ny = ny; o.gridx = gx; o.gridy = gy; o.tblock = K; o.boundary = boundary;
+  o.periodic_x = px; o.periodic_y = py; o.device = -1; o.convergence = conv; o.interval = 6; o.sensitivity = 1e-30;
+  o.poison = true;
+  Engine e(o);
+  RunStats st = e.run(29);
+  st = e.run(8);  // a second run continues the chunk schedule
+  Physics ph; ph.boundary = boundary; ph.periodic_x = px; ph.periodic_y = py;
+  OracleResult r = oracle_run(nx, ny, 37, ph, kInitExact, conv, 6, 1e-30, nullptr);
+  for (int t = 0; t < e.num_tiles(); ++t) {
+    const TileGeom g = e.geom(t);
+    std::vector<float> b = e.download(t);
+    for (int64_t i = 0; i < g.xcell; ++i)
+      if (std::memcmp(&b[i * g.ycell], &r.grid[(g.gx0 + i) * ny + g.gy0], g.ycell * sizeof(float))) return 1;
+  }
+  return st.steps_done == 37 ? 0 : 2;
+}
+int main() {
+  int bad = 0;
+  bad += check_engine(41, 37, 3, 2, 5, kFixed, false, false, false);
+  bad += check_engine(30, 44, 2, 2, 4, kGhostZero, true, true, true);
+  bad += check_engine(25, 19, 1, 3, 3, kGhostZero, false, true, false);
+  // the unit planner (host code shared with the GPU path)
+  for (int K : {1, 4, 8, 16}) {
+    for (int64_t nx : {1, 9, 100, 513}) for (int64_t ny : {1, 255, 256, 700, 4096}) {
+      TileGeom g = make_tile_geom(nx, ny, 0, 0, nx, ny, K);
+      bool peer[kNumDirs] = {true, true, false, false, false, false, false, false};
+      for (int64_t cap : {1, 64, 1024}) {
+        UnitPlan p = plan_units(g, K, 0, true, false, false, 1.2, cap, peer, 8);
+        std::vector<Unit> u = build_units(g, K, 0, false, true, false, 1.0, cap);
+        int64_t rows = 0;
+        for (const Unit& x : u) rows += x.h;
+        std::vector<Strip> s = strip_layout(g, K, true, false);
+        if (rows != nx * (int64_t)strip_layout(g, K, false, false).size()) bad += 100;
+        (void)p; (void)s;
+      }
+    }
+  }
+  std::printf("ok %d\n", bad);
+  return bad;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"), reason="no hipcc")
+def test_host_sanitizers_engine_cpu_path(native, tmp_path):
+    """The engine's CPU path (chunk scheduler, local halo plans, poison canary, convergence) and
+    the work-unit planner under ASan + UBSan, with every -fsanitize= behind -Xarch_host (host
+    code only; nothing runs on a GPU: the engine is created with device = -1).  The heavy
+    stencil translation units (device code only, unchanged) are linked from the regular build."""
+    import concurrent.futures as cf
+
+    from heat2d_amd import _build
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    csrc = os.path.join(ROOT, "heat2d_amd", "csrc")
+    drv = tmp_path / "engine_san.cpp"
+    drv.write_text(ENGINE_SAN_DRIVER)
+    srcs = [str(drv)] + [os.path.join(csrc, f) for f in ("engine.cpp", "decomposition.cpp", "cpu_reference.cpp",
+                                                          "kernels.hip")]
+    prebuilt = [_build._obj_for(f) for f in ["tile_kernel.hip"] + [f"stream_k{k}.hip" for k in
+                                                                    (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16)]]
+    assert all(os.path.exists(o) for o in prebuilt)
+    flags = ["-x", "hip", "--offload-arch=gfx950", "-std=c++17", "-O1", "-ffp-contract=off", f"-I{csrc}",
+             "-Xarch_host", "-g", "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-sanitize-recover=all", "-Xarch_host", "-fno-omit-frame-pointer"]
+
+    def compile_one(src):
+        obj = str(tmp_path / (os.path.basename(src) + ".o"))
+        r = subprocess.run([hipcc, *flags, "-c", src, "-o", obj], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return obj
+
+    with cf.ThreadPoolExecutor(min(8, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    exe = str(tmp_path / "engine_san")
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-fsanitize=address,undefined", *objs, *prebuilt, "-o", exe,
+                        "-L/opt/rocm/lib", "-lrccl", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0 and r.stdout.startswith("ok 0"), r.stdout[-2000:] + r.stderr[-4000:]
