@@ -153,18 +153,21 @@ def main() -> int:
             sync()
 
     # ---- pre-warm (untimed, time-based, collectively agreed count) + W warm-up steps --------
+    # The pre-warm replays the timed run's exact shape (runs of K steps: the same chunk depths,
+    # so the same kernel code is hot in the caches) until the GPU has been busy ~prewarm_s.
     run = s.run_steps
     prewarm_steps = 0
-    if on_gpu and a.prewarm_s > 0:
+    if on_gpu and a.prewarm_s > 0 and a.steps > 0:
         # ranks that ran different step counts would post unmatched halo sends and deadlock
         sync_barrier()
         t0 = time.perf_counter()
-        run(64)
+        run(a.steps)
         sync_barrier()
         t_batch = ctx.allreduce_max(time.perf_counter() - t0)
-        batches = max(0, min(100000, math.ceil(a.prewarm_s / max(t_batch, 1e-6)) - 1))
-        run(64 * batches)
-        prewarm_steps = 64 * (batches + 1)
+        batches = max(0, min(20000, math.ceil(a.prewarm_s / max(t_batch, 1e-6)) - 1))
+        for _ in range(batches):
+            run(a.steps)
+        prewarm_steps = a.steps * (batches + 1)
         sync_barrier()
     if a.warmup > 0:
         run(a.warmup)
@@ -201,8 +204,14 @@ def main() -> int:
             e = n.Engine(rnx, rny, boundary=0 if a.boundary == "fixed" else 1,
                          precision=0 if a.precision == "ref" else 1, tblock=a.tblock,
                          rows_per_wave=a.rows_per_wave, device=device, small_grid_lds=False)
-            pre = prewarm_steps + max(0, a.warmup)
-            e.run(pre) if pre > 0 else None
+            # the same step count as the multi-GPU run, its last pre-warm run shaped like the timed one
+            if prewarm_steps >= a.steps:
+                e.run(prewarm_steps - a.steps) if prewarm_steps > a.steps else None
+                e.run(a.steps)
+            elif prewarm_steps > 0:
+                e.run(prewarm_steps)
+            if a.warmup > 0:
+                e.run(a.warmup)
             ts = []
             for _ in range(max(1, a.repeat)):
                 e.synchronize()

@@ -84,10 +84,23 @@ __device__ __forceinline__ float4 row_update(const float4& P, const float4& C, c
   const float ew0 = from_left(C.w) + C.y;
   const float ew3 = C.z + from_right(C.x);
   float4 o;
-  o.x = cell<F32>(C.x, sn01.x, ew0, k);
-  o.y = cell<F32>(C.y, sn01.y, ew12.x, k);
-  o.z = cell<F32>(C.z, sn23.x, ew12.y, k);
-  o.w = cell<F32>(C.w, sn23.y, ew3, k);
+  if constexpr (F32) {
+    // fp32 fast path: two cells per packed FMA (v_pk_fma_f32: each half is an IEEE fma, so the
+    // values equal cell<true> / update_f32 bit for bit) — 4 instead of 8 FMAs per cell pair
+    const f32x2 c01 = {C.x, C.y}, c23 = {C.z, C.w};
+    const f32x2 ew01 = {ew0, ew12.x}, ew23 = {ew12.y, ew3};
+    const f32x2 m2 = {-2.0f, -2.0f}, cx2 = {k.cxf, k.cxf}, cy2 = {k.cyf, k.cyf};
+    f32x2 r01 = __builtin_elementwise_fma(cx2, __builtin_elementwise_fma(m2, c01, sn01), c01);
+    f32x2 r23 = __builtin_elementwise_fma(cx2, __builtin_elementwise_fma(m2, c23, sn23), c23);
+    r01 = __builtin_elementwise_fma(cy2, __builtin_elementwise_fma(m2, c01, ew01), r01);
+    r23 = __builtin_elementwise_fma(cy2, __builtin_elementwise_fma(m2, c23, ew23), r23);
+    o = make_float4(r01.x, r01.y, r23.x, r23.y);
+  } else {
+    o.x = cell<F32>(C.x, sn01.x, ew0, k);
+    o.y = cell<F32>(C.y, sn01.y, ew12.x, k);
+    o.z = cell<F32>(C.z, sn23.x, ew12.y, k);
+    o.w = cell<F32>(C.w, sn23.y, ew3, k);
+  }
   return o;
 }
 
