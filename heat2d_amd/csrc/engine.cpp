@@ -848,6 +848,7 @@ void Engine::exchange_landed() {
 std::string Engine::pipeline() const {
   if (!has_exchange_) return "none";
   if (direct_) return "direct";
+  if (transport_ == kTransportExternal) return "external";
   if (sig_mode_ > 0) return "signal";
   if (concurrent_) return opt_.comm_boundary != 0 ? "concurrent" : "concurrent3";
   return opt_.overlap ? "boundary-first" : "serial";

@@ -16,6 +16,10 @@
 #include <sys/stat.h>
 #include <vector>
 
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include "bootstrap.h"
 #include "cpu_reference.h"
 #include "decomposition.h"
 #include "engine.h"
@@ -66,24 +70,130 @@ const std::map<std::string, Preset>& presets() {
                "              [--cx X] [--cy X] [--boundary fixed|ghost-zero] [--init exact|ref-int32|zero]\n"
                "              [--precision ref|fp32] [--periodic none|x|y|xy] [--output auto|text|binary|both|none]\n"
                "              [--outdir DIR] [--device gpu|cpu] [--tblock K] [--rows-per-wave H] [--no-overlap]\n"
-               "              [--numthreads N] [--debug 0|1] [--json] [--quiet]\n");
+               "              [--numthreads N] [--debug 0|1] [--json] [--quiet]\n"
+               "              [--np P]   run P ranks (forked here, like mpiexec -n P; or launch with\n"
+               "                         torch.distributed.run --no-python: RANK/WORLD_SIZE/MASTER_ADDR)\n");
   std::exit(2);
 }
 
-void write_outputs(Engine& e, const std::string& outdir, const char* which, int64_t NX, int64_t NY, bool binary,
-                   bool text, int style) {
+void write_outputs(Engine& e, Bootstrap& boot, const std::string& outdir, const char* which, int64_t NX, int64_t NY,
+                   bool binary, bool text, int style) {
+  // every rank pwrites its own tile rows into the global raw file (the MPI-IO file view the
+  // reference intended, B-3); rank 0 creates it first and converts it to text last
   if (!binary && !text) return;
-  ::mkdir(outdir.c_str(), 0755);
   const std::string bin = outdir + "/" + which + "_binary.dat";
   const std::string tmp = binary ? bin : outdir + "/." + which + "_binary.tmp";
-  binary_create(tmp, NX, NY);
+  if (boot.rank() == 0) {
+    ::mkdir(outdir.c_str(), 0755);
+    binary_create(tmp, NX, NY);
+  }
+  boot.barrier();
   for (int t = 0; t < e.num_tiles(); ++t) {
     const TileGeom g = e.geom(t);
     const std::vector<float> b = e.download(t);
     binary_write_tile(tmp, NX, NY, g.gx0, g.gy0, g.xcell, g.ycell, b.data());
   }
-  if (text) binary_to_text(tmp, outdir + "/" + which + ".dat", NX, NY, style);
-  if (!binary) std::remove(tmp.c_str());
+  boot.barrier();
+  if (boot.rank() == 0) {
+    if (text) binary_to_text(tmp, outdir + "/" + which + ".dat", NX, NY, style);
+    if (!binary) std::remove(tmp.c_str());
+  }
+  boot.barrier();
+}
+
+// `heat2d --np P ...`: the mpiexec of this program.  Forks P ranks BEFORE anything touches a
+// GPU (each child execs this binary with RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR set),
+// waits for all of them, and returns the first failure.
+int launch_ranks(int np, int argc, char** argv) {
+  std::vector<std::string> args;
+  for (int i = 0; i < argc; ++i) {
+    if (std::string(argv[i]) == "--np") {
+      ++i;
+      continue;
+    }
+    args.push_back(argv[i]);
+  }
+  const int port = 20000 + (int)(::getpid() % 20000);
+  std::vector<pid_t> kids;
+  for (int r = 0; r < np; ++r) {
+    const pid_t pid = ::fork();
+    if (pid < 0) {
+      std::perror("heat2d: fork");
+      return 1;
+    }
+    if (pid == 0) {
+      ::setenv("RANK", std::to_string(r).c_str(), 1);
+      ::setenv("LOCAL_RANK", std::to_string(r).c_str(), 1);
+      ::setenv("WORLD_SIZE", std::to_string(np).c_str(), 1);
+      ::setenv("MASTER_ADDR", "127.0.0.1", 1);
+      ::setenv("HEAT2D_BOOT_PORT", std::to_string(port).c_str(), 1);
+      std::vector<char*> cargv;
+      for (auto& x : args) cargv.push_back(const_cast<char*>(x.c_str()));
+      cargv.push_back(nullptr);
+      ::execv("/proc/self/exe", cargv.data());
+      std::perror("heat2d: exec");
+      std::_Exit(127);
+    }
+    kids.push_back(pid);
+  }
+  int rc = 0;
+  for (pid_t k : kids) {
+    int st = 0;
+    ::waitpid(k, &st, 0);
+    const int c = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+    if (c != 0 && rc == 0) rc = c;
+  }
+  return rc;
+}
+
+// The CPU multi-rank time loop: the engine's external transport, halos relayed through the
+// bootstrap star (pack -> exchange -> unpack), the convergence sum over ranks in rank order.
+RunStats run_external(Engine& e, Bootstrap& boot, int64_t steps, double sensitivity) {
+  RunStats st;
+  st.path = "cpu";
+  const int me = boot.rank();
+  const int64_t total = e.steps_done() + steps;
+  int64_t done = e.steps_done();
+  while (done < total) {
+    bool check = false;
+    const int k = e.next_chunk(done, total, &check);
+    const std::vector<int64_t> info = e.plan_info(0, k);  // [peer, send_off, send_n, recv_off, recv_n] x 8
+    std::vector<float> sb((size_t)std::max<int64_t>(1, e.send_count(0, k)));
+    std::vector<float> rb((size_t)std::max<int64_t>(1, e.recv_count(0, k)));
+    e.pack(0, k, reinterpret_cast<uintptr_t>(sb.data()));
+    std::vector<Bootstrap::Msg> out;
+    for (int d = 0; d < kNumDirs; ++d) {
+      const int64_t peer = info[5 * d], so = info[5 * d + 1], sn = info[5 * d + 2];
+      if (peer >= 0 && sn > 0)
+        out.push_back({(int)peer, d, std::string(reinterpret_cast<const char*>(sb.data() + so), (size_t)sn * 4)});
+    }
+    const auto in = boot.exchange(out);
+    for (int d = 0; d < kNumDirs; ++d) {
+      const int g = kDirOpp[d];  // ghost side g receives the segment its peer sent in direction d
+      const int64_t peer = info[5 * g], ro = info[5 * g + 3], rn = info[5 * g + 4];
+      if (peer < 0 || rn <= 0) continue;
+      auto it = in.find(std::make_pair((int)peer, d));
+      if (it == in.end() || it->second.size() != (size_t)rn * 4)
+        throw std::runtime_error("rank " + std::to_string(me) + ": halo segment missing");
+      std::memcpy(rb.data() + ro, it->second.data(), (size_t)rn * 4);
+    }
+    e.unpack(0, k, reinterpret_cast<uintptr_t>(rb.data()));
+    ++st.exchanges;
+    e.advance(k, check);
+    ++st.chunks;
+    if (check) {
+      st.residual = boot.allreduce_sum(e.local_residual());
+      if (st.residual < sensitivity) {
+        e.rollback();
+        st.converged = true;
+        break;
+      }
+    }
+    done += k;
+  }
+  e.set_steps_done(done);
+  st.steps_done = done;
+  return st;
 }
 
 }  // namespace
@@ -102,6 +212,9 @@ int main(int argc, char** argv) {
     a[k] = argv[++i];
   }
   if (a.count("help")) usage(nullptr);
+  if (a.count("np") && std::atoi(a["np"].c_str()) > 1) return launch_ranks(std::atoi(a["np"].c_str()), argc, argv);
+  const RankEnv env = rank_env();
+  const int world = env.world;
   const std::string pname = a.count("preset") ? a["preset"] : "heat2d";
   if (!presets().count(pname)) usage("unknown preset");
   const Preset P = presets().at(pname);
@@ -114,9 +227,14 @@ int main(int argc, char** argv) {
   const int64_t steps = geti("steps", P.steps);
   o.gridx = (int)geti("gridx", P.gridx);
   o.gridy = (int)geti("gridy", P.gridy);
-  if (o.gridx == 0) o.gridx = 1;  // automatic: the world size, one process here
-  if (o.gridx < 1 || o.gridy < 1) usage("gridx/gridy must be >= 1 in the single-process program");
   if (P.strips && !a.count("gridy")) o.gridy = 1;
+  if (o.gridx == 0) o.gridx = std::max(1, world / std::max(1, o.gridy));  // automatic: strips over the ranks
+  if (o.gridx < 1 || o.gridy < 1) usage("gridx/gridy must be >= 1");
+  if (world > 1 && o.gridx * o.gridy != world) {
+    if (env.rank == 0)
+      std::printf("ERROR: the number of tasks must be equal to %d.\nQuiting...\n", o.gridx * o.gridy);
+    return 1;
+  }
   o.convergence = geti("convergence", P.convergence ? 1 : 0) != 0;
   o.interval = geti("interval", P.interval);
   o.sensitivity = getd("sensitivity", P.sensitivity);
@@ -137,9 +255,19 @@ int main(int argc, char** argv) {
   if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
   const std::string dev = a.count("device") ? a["device"] : (ndev > 0 ? "gpu" : "cpu");
   if (dev == "gpu" && ndev == 0) usage("--device gpu but no HIP device is visible");
-  o.device = dev == "gpu" ? 0 : -1;
+  o.device = dev == "gpu" ? env.local_rank % std::max(1, ndev) : -1;
   o.transport = kTransportLocal;
-  const bool quiet = a.count("quiet") > 0;
+  // multi-rank: one tile per process; GPUs: the direct IPC halo pipeline for 1-D row strips,
+  // RCCL otherwise; CPUs: halos relayed through the bootstrap
+  const bool rows = o.gridy == 1 && !o.periodic_y;
+  const std::string tsel = a.count("transport") ? a["transport"] : "auto";
+  if (world > 1) {
+    o.ranks = {env.rank};
+    if (dev != "gpu") o.transport = kTransportExternal;
+    else if ((tsel == "auto" || tsel == "ipc") && rows) o.transport = kTransportIpc;
+    else o.transport = kTransportRccl;
+  }
+  const bool quiet = a.count("quiet") > 0 || env.rank != 0;
   std::string output = a.count("output") ? a["output"] : "auto";
   if (output == "auto") {
     const bool t = P.text != "none";
@@ -152,7 +280,16 @@ int main(int argc, char** argv) {
   const std::string rep = P.report;
 
   try {
+    Bootstrap boot(env.rank, world, env.addr, env.port);
     Engine e(o);
+    if (o.transport == kTransportIpc && e.has_exchange()) {
+      e.ipc_open(boot.allgather(e.ipc_handle()));
+      boot.barrier();
+      e.ipc_prime();
+      boot.barrier();
+    } else if (o.transport == kTransportRccl && e.has_exchange()) {
+      e.init_rccl(boot.broadcast(env.rank == 0 ? Engine::rccl_unique_id() : std::string()), world, env.rank);
+    }
     const Decomposition& d = e.decomposition();
     const int nprocs = d.nranks();
     if (!quiet) {
@@ -186,16 +323,19 @@ int main(int argc, char** argv) {
     }
     if (output != "none") {
       if (!quiet && (rep == "grad" || rep == "hybrid")) std::printf("Writing initial.dat ...\n");
-      write_outputs(e, outdir, "initial", o.nx, o.ny, wbin, wtxt, tstyle);
+      write_outputs(e, boot, outdir, "initial", o.nx, o.ny, wbin, wtxt, tstyle);
     }
     if (!quiet && rep == "heat2dn")
       for (int i = 0; i < d.gridx; ++i) std::printf("Task %d received work. Beginning time steps...\n", i + 1);
     std::fflush(stdout);
     e.synchronize();
+    boot.barrier();
     const auto t0 = std::chrono::steady_clock::now();
-    const RunStats st = e.run(steps);
+    const RunStats st = o.transport == kTransportExternal && e.has_exchange() ? run_external(e, boot, steps, o.sensitivity)
+                                                                             : e.run(steps);
     e.synchronize();
-    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    // the loop's wall time, max over ranks (grad1612_mpi_heat.c:277-280)
+    const double el = boot.allreduce_max(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     if (!quiet) {
       if (rep == "grad" || rep == "hybrid") {
         std::printf("Exiting after %lld iterations\nElapsed time: %e sec\n", (long long)st.steps_done, el);
@@ -209,13 +349,14 @@ int main(int argc, char** argv) {
         std::printf("Elapsed time: %e sec\n", el);
       }
     }
-    if (output != "none") write_outputs(e, outdir, "final", o.nx, o.ny, wbin, wtxt, tstyle);
-    if (a.count("json")) {
+    if (output != "none") write_outputs(e, boot, outdir, "final", o.nx, o.ny, wbin, wtxt, tstyle);
+    if (a.count("json") && env.rank == 0) {
       const double cups = el > 0 ? (double)o.nx * (double)o.ny * (double)st.steps_done / el : 0.0;
       std::printf("{\"grid\": [%lld, %lld], \"steps\": %lld, \"elapsed_s\": %.9g, \"cell_updates_per_s\": %.9g, "
-                  "\"path\": \"%s\", \"device\": \"%s\", \"tiles\": %d, \"converged\": %s, \"chunks\": %lld}\n",
+                  "\"path\": \"%s\", \"device\": \"%s\", \"tiles\": %d, \"ranks\": %d, \"pipeline\": \"%s\", "
+                  "\"converged\": %s, \"chunks\": %lld}\n",
                   (long long)o.nx, (long long)o.ny, (long long)st.steps_done, el, cups, st.path.c_str(), dev.c_str(),
-                  e.num_tiles(), st.converged ? "true" : "false", (long long)st.chunks);
+                  e.num_tiles(), world, e.pipeline().c_str(), st.converged ? "true" : "false", (long long)st.chunks);
     }
   } catch (const std::exception& ex) {
     std::fprintf(stderr, "heat2d: error: %s\n", ex.what());

@@ -87,3 +87,22 @@ def test_gpu_bench_two_ranks_host_transport(tmp_path):
     assert d["n_gpus"] == 2 and d["steps"] == 40 and d["config"]["grid"] == [1024, 1024]
     assert d["value"] > 0 and d["config"]["transport"] == "host" and d["scaling"] == "strong"
     assert d["gate"][0]["ok"] and d["verified"] is True and d["speedup"] > 0
+
+
+@pytest.mark.parametrize("n,conv", [(2, 0), (3, 1)])
+def test_native_cli_ranks_ipc_on_gpu(native, gpu, tmp_path, n, conv):
+    """The native executable's own launcher (`heat2d --np P`) on the GPU: ranks share the card
+    through the direct IPC halo pipeline; bit-exact against the oracle."""
+    exe = os.path.join(ROOT, "heat2d_amd", "bin", "heat2d")
+    nx, ny, steps = 70 * n + 3, 517, 41
+    args = [exe, "--np", str(n), "--device", "gpu", "--nx", str(nx), "--ny", str(ny), "--steps", str(steps),
+            "--gridx", str(n), "--gridy", "1", "--output", "binary", "--outdir", str(tmp_path), "--json"]
+    kw = {}
+    if conv:
+        args += ["--convergence", "1", "--interval", "6", "--sensitivity", "1e-30"]
+        kw = dict(convergence=True, interval=6, sensitivity=1e-30)
+    r = subprocess.run(args, cwd=str(tmp_path), env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert '"pipeline": "direct"' in r.stdout and f'"ranks": {n}' in r.stdout
+    ref = native.oracle_run(nx, ny, steps, **kw)["grid"]
+    assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
