@@ -427,7 +427,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   // whatever this chunk's K: they must cover (and release) at least G_ rows.
   const int hb = std::max(opt_.boundary_rows, G_);
   UnitPlan P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
-                          opt_.edge_weight, cap, peer, hb);
+                          opt_.edge_weight, cap, peer, hb, opt_.row_edge_weight);
   // auto headroom (4096^2 row-periodic RCCL self-exchange, us/step: 14.3 -> 10.4-10.9 with
   // 16 in the concurrent pipeline; 14.3 -> 12.6 with 32 in the boundary-first one)
   const int64_t reserve = opt_.reserve_waves >= 0 ? opt_.reserve_waves : ((concurrent_ || sig_mode_ > 0) ? 16 : 32);
@@ -437,7 +437,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     const int64_t nb = (concurrent_ || sig_mode_ > 0) ? (int64_t)P.boundary.size() : 0;
     const int64_t cap_in = std::max<int64_t>(cap / 2, cap - nb - reserve);
     P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
-                   opt_.edge_weight, cap_in, peer, hb);
+                   opt_.edge_weight, cap_in, peer, hb, opt_.row_edge_weight);
   }
   // Signalled pipeline with only north/south peers (1-D row strips): no short boundary units.
   // Every strip is cut into capacity-fitted units as if the tile had no peers; the top unit
@@ -463,7 +463,8 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     if (attempt == 1 && ew == opt_.edge_weight) continue;
     if (attempt == 2 && Hq == opt_.rows_per_wave) break;
     UnitPlan Q = plan_units(g, K, Hq, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
-                            ew, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, hb);
+                            ew, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, hb,
+                            attempt == 0 ? opt_.row_edge_weight : 1.0);
     std::map<int, std::pair<int, int>> ends;  // strip -> (top unit, bottom unit) indices
     for (int i = 0; i < (int)Q.interior.size(); ++i) {
       const Unit& u = Q.interior[i];

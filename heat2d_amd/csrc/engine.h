@@ -52,7 +52,8 @@ struct EngineOptions {
   double cx = kCxDouble, cy = kCxDouble;
   int tblock = 8;          // max fused steps per chunk (= halo depth)
   int rows_per_wave = 0;   // H; 0 = automatic
-  double edge_weight = 1.2;  // relative cost of a global-edge work unit (load balance)
+  double edge_weight = 1.2;      // relative cost of a column-edge work unit (load balance)
+  double row_edge_weight = -1.0;  // ... of a row-edge unit (<= 0: edge_weight)
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   int boundary_rows = 8;      // rows per halo-dependent work unit (overlap mode; at least K)
   int concurrent = -1;        // boundary units on a second stream: -1 auto, 0 never, 1 always

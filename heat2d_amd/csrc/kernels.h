@@ -60,8 +60,9 @@ std::vector<Unit> build_units(const TileGeom& g, int K, int H, bool fixed, bool 
 struct UnitPlan {
   std::vector<Unit> interior, boundary;
 };
+// row_edge_weight: the cost weight of units whose cone reaches a global edge ROW (<= 0: edge_weight)
 UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
-                    int64_t capacity, const bool* peer, int hb);
+                    int64_t capacity, const bool* peer, int hb, double row_edge_weight = -1.0);
 // Resident waves of the streaming kernel on `device` (occupancy query × CUs × 4 waves/block).
 int64_t stream_wave_capacity(int K, int precision, int device);
 

@@ -349,9 +349,13 @@ struct RowRange {
 // edge unit costs w times more: target cost U -> h = U - K (plain) or U/w - K (edge).
 std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>& strips,
                               const std::vector<RowRange>& ranges, int H, bool fixed, bool per_x, bool per_y,
-                              double edge_weight, int64_t capacity) {
+                              double edge_weight, int64_t capacity, double row_edge_weight) {
+  // edge units cost more per row: column-edge strips run the column-masked body on every row,
+  // row-edge units (their K-cone reaches a global edge row) the row-masked one
   const double w = std::max(1.0, edge_weight);
+  const double wr = std::max(1.0, row_edge_weight > 0 ? row_edge_weight : edge_weight);
   auto rows_for = [&](double U, bool edge) { return std::max<int64_t>(1, (int64_t)(edge ? U / w - K : U - K)); };
+  auto rows_row_edge = [&](double U) { return std::max<int64_t>(1, (int64_t)(U / wr - K)); };
   auto plan = [&](double U, std::vector<Unit>* out) -> int64_t {
     int64_t count = 0;
     auto emit = [&](int64_t strip, int64_t a, int64_t b, int64_t target) {
@@ -370,7 +374,7 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
     };
     for (const RowRange& r : ranges) {
       int64_t a = r.a, b = r.b;
-      const int64_t he = rows_for(U, true);
+      const int64_t he = rows_row_edge(U);
       if (r.edge_top && b > a) {
         const int64_t e = std::min(b, a + he);
         emit(r.strip, a, e, he);
@@ -392,7 +396,7 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
     // Minimise the estimated makespan ceil(units / capacity) * U: one full round when the
     // tile has few strips (the usual case); several full rounds for huge tiles whose strips
     // alone outnumber the resident waves.  Units never go below 8 rows.
-    const double umin = 8.0 + K, umax = (double)(g.xcell + K) * w + 1.0;
+    const double umin = 8.0 + K, umax = (double)(g.xcell + K) * std::max(w, wr) + 1.0;
     double best_u = umax, best_ms = 1e300;
     for (double u = umin; u <= umax * 1.0001; u *= 1.03) {
       const int64_t cnt = plan(u, nullptr);
@@ -411,7 +415,7 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
 }  // namespace
 
 UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
-                    int64_t capacity, const bool* peer, int hb) {
+                    int64_t capacity, const bool* peer, int hb, double row_edge_weight) {
   UnitPlan P;
   const std::vector<Strip> strips = strip_layout(g, K, fixed, per_y);
   const int64_t nstrips = (int64_t)strips.size();
@@ -446,9 +450,9 @@ UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, boo
       in_r.push_back(RowRange{s, top, bot, col_edge});
     }
   }
-  P.interior = size_ranges(g, K, strips, in_r, H, fixed, per_x, per_y, edge_weight, capacity);
+  P.interior = size_ranges(g, K, strips, in_r, H, fixed, per_x, per_y, edge_weight, capacity, row_edge_weight);
   // Boundary units are short (hb rows): they run first, alone, and gate the halo exchange.
-  P.boundary = size_ranges(g, K, strips, bd_r, hb, fixed, per_x, per_y, 1.0, capacity);
+  P.boundary = size_ranges(g, K, strips, bd_r, hb, fixed, per_x, per_y, 1.0, capacity, 1.0);
   auto edge_first = [](const Unit& a, const Unit& b) { return (a.flags != 0) > (b.flags != 0); };
   std::stable_sort(P.interior.begin(), P.interior.end(), edge_first);
   return P;
