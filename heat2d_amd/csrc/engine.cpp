@@ -295,11 +295,10 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     const bool self_only = tiles_.size() == 1 && transport_ == kTransportLocal;
     if (self_only && !opt_.naive && opt_.tiled != 0) {
       const int64_t NX = dec_.NX, NY = dec_.NY;
-      // Auto: the tiled path up to 640x512-class grids; the whole-grid LDS solver keeps
-      // convergence runs that fit it (its check needs no host round trip).  Measured on
-      // MI355X, ref precision, 1000 steps (profiles/tile_sweep_r1.txt), us/step
-      // tiled / LDS solver / streaming: 80x64 0.90 / 1.56 / 1.60; 160x128 0.87 / 4.05 / 1.63;
-      // 320x256 0.91 / - / 1.61; 640x512 1.36 / - / 1.89; 1280x1024 2.50 / - / 2.07.
+      // Auto: the tiled path up to 640x512-class grids.  Measured on MI355X, ref precision,
+      // 1000 steps (profiles/tile_sweep_r2.txt), us/step tiled / LDS solver / streaming:
+      // 80x64 0.49 / 1.58 / 1.57; 160x128 0.55 / 4.08 / 1.59; 320x256 0.65 / - / 1.55;
+      // 640x512 0.96 / - / 1.86; 1280x1024 2.08 / - / 2.11 (streaming kept above 600k cells).
       const int64_t cells = NX * NY;
       // (with the fused device-side check the tiled path converges without host round trips
       // too, and is faster per step: it no longer yields to the whole-grid solver)
@@ -307,18 +306,39 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
           opt_.small_grid_lds && !has_exchange_ && lds_solver_fits(NX, NY) && opt_.convergence && !fused_;
       const bool want = opt_.tiled == 1 || (cells <= 600000 && !lds_whole);
       if (want && NX < (1 << 30) && NY < (1 << 30)) {
-        int RY = opt_.tile_width > 0 ? opt_.tile_width : 64;
-        if (RY != 64 && RY != 128) throw std::invalid_argument("tile_width must be 64 or 128");
-        int K = opt_.tile_k > 0 ? opt_.tile_k : (cells <= 32768 ? 16 : 8);
+        // Automatic shape by grid size (tools/tile_sweep.py on MI355X, ref precision, us/step,
+        // profiles/tile_sweep_r2.txt): small regions of many workgroups, 1024 threads, few cells
+        // per lane — the launch is latency-bound (per-level LDS round trip + barrier), not VALU-bound.
+        struct AutoTile {
+          int64_t max_cells;
+          int ry, k, tx, nt, cpl;
+        };
+        static const AutoTile kAuto[] = {
+            {10240, 32, 16, 8, 1024, 1},    // 80x64: 0.49
+            {40960, 64, 16, 4, 1024, 2},    // 160x128: 0.55
+            {163840, 64, 16, 16, 1024, 4},  // 320x256: 0.65
+            {INT64_MAX, 128, 16, 16, 1024, 4},  // 640x512: 0.96
+        };
+        const AutoTile* at = kAuto;
+        while (cells > at->max_cells) ++at;
+        int RY = opt_.tile_width > 0 ? opt_.tile_width : at->ry;
+        if (RY != 32 && RY != 64 && RY != 128) throw std::invalid_argument("tile_width must be 32, 64 or 128");
+        int K = opt_.tile_k > 0 ? opt_.tile_k : at->k;
         K = std::max(1, std::min(K, (RY - 4) / 2));
-        int TX = opt_.tile_rows;
-        if (TX <= 0) TX = cells <= 131072 ? 8 : 16;
-        while (TX > 1 && !tile_config_ok(TX, RY, K)) TX /= 2;
-        if (!tile_config_ok(TX, RY, K)) throw std::invalid_argument("no valid LDS tile configuration");
+        int TX = opt_.tile_rows > 0 ? opt_.tile_rows : at->tx;
+        int CPL = opt_.tile_cpl > 0 ? opt_.tile_cpl : at->cpl;
+        if (CPL != 1 && CPL != 2 && CPL != 4) throw std::invalid_argument("tile_cpl must be 1, 2 or 4");
+        while (CPL < 4 && RY / CPL > 64) CPL *= 2;  // a region row must fit one wave
+        const int NT = opt_.tile_threads > 0 ? opt_.tile_threads : at->nt;
+        if (NT != 256 && NT != 1024) throw std::invalid_argument("tile_threads must be 256 or 1024");
+        while (TX > 1 && !tile_config_ok(TX, RY, K, CPL, NT)) TX /= 2;
+        if (!tile_config_ok(TX, RY, K, CPL, NT)) throw std::invalid_argument("no valid LDS tile configuration");
         tiled_ = true;
         tile_tx_ = TX;
         tile_ry_ = RY;
         tile_k_ = K;
+        tile_cpl_ = CPL;
+        tile_nt_ = NT;
         Tile& T = tiles_[0];
         const int64_t need = tile_count((int)NX, (int)NY, TX, RY - 2 * K);
         if (need > T.pcap) {
@@ -1050,6 +1070,8 @@ RunStats Engine::run_impl(int64_t steps) {
       a.NX = (int)T.g.xcell;
       a.NY = (int)T.g.ycell;
       a.TX = tile_tx_;
+      a.NT = tile_nt_;
+      a.CPL = tile_cpl_;
       a.RY = tile_ry_;
       a.K = k;
       a.TY = tile_ry_ - 2 * k;

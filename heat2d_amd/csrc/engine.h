@@ -103,10 +103,12 @@ struct EngineOptions {
   bool overlap = true;     // overlap halo exchange with interior compute
   bool small_grid_lds = true;  // whole-grid LDS solver for small single-tile problems
   // LDS-tiled temporally-blocked kernel (tile_kernel.hip) for single-tile runs of small and
-  // medium grids: -1 auto (by size), 0 off, 1 on.  tile_rows = TX, tile_width = RY (64 or
-  // 128 region columns), tile_k = steps per launch; 0 = automatic.
+  // medium grids: -1 auto (by size), 0 off, 1 on.  tile_rows = TX, tile_width = RY (32, 64
+  // or 128 region columns), tile_k = steps per launch; 0 = automatic.
   int tiled = -1;
   int tile_rows = 0, tile_width = 0, tile_k = 0;
+  int tile_threads = 0;  // workgroup size of the tiled kernel: 256, 1024, 0 = automatic
+  int tile_cpl = 0;      // cells per lane and level of the tiled kernel: 1, 2, 4, 0 = automatic
   bool naive = false;      // validation: one-thread-per-cell single-step kernel
   // CUs reserved for the comm stream (pack/unpack/RCCL kernels) when halos are exchanged;
   // the compute streams are masked to the other CUs so the exchange kernels never wait for
@@ -156,6 +158,8 @@ class Engine {
   int signal_mode() const { return sig_mode_; }
   bool tiled() const { return tiled_; }
   std::vector<int> tile_config() const { return {tile_tx_, tile_ry_, tile_k_}; }
+  int tile_threads() const { return tile_nt_; }
+  int tile_cpl() const { return tile_cpl_; }
   // "none" (no exchange), "signal", "concurrent", "concurrent3", "boundary-first", "serial"
   std::string pipeline() const;
   int rows_per_wave(int K) const;  // largest unit height for depth K (tile 0)
@@ -282,7 +286,7 @@ class Engine {
   int comm_cus_ = 0, device_cus_ = 0;
   bool contig_ = false;
   bool tiled_ = false;                      // resolved EngineOptions::tiled
-  int tile_tx_ = 0, tile_ry_ = 0, tile_k_ = 0;
+  int tile_tx_ = 0, tile_ry_ = 0, tile_k_ = 0, tile_nt_ = 256, tile_cpl_ = 4;
   int sig_mode_ = 0;                        // resolved signal_exchange
   unsigned long long* sig_counter_ = nullptr;  // boundary units completed (cumulative)
   unsigned long long sig_target_ = 0;          // boundary units launched (cumulative, host)

@@ -5,14 +5,16 @@
 
 namespace h2d {
 
-// Arguments of the LDS-tiled temporally-blocked kernel (tile_kernel.hip): one 256-thread
-// workgroup per TX x TY tile, K steps per launch, region RY = TY + 2K columns (64 or 128).
+// Arguments of the LDS-tiled temporally-blocked kernel (tile_kernel.hip): one NT-thread
+// workgroup per TX x TY tile, K steps per launch, region RY = TY + 2K columns (32, 64 or 128).
 struct TileArgs {
   const float* src;  // owned cell (0, 0) of the single tile (whole grid)
   float* dst;
   int64_t pitch;
   int NX, NY;
   int TX, TY, RY, K;
+  int NT = 256;  // threads per workgroup: 256 or 1024
+  int CPL = 4;   // cells per lane and level: 1, 2 or 4 (RY / CPL <= 64: a region row in one wave)
   int tiles_y = 0, ntiles = 0;  // set by launch_tile
   double cx, cy;
   int fixed, per_x, per_y;
@@ -22,7 +24,9 @@ struct TileArgs {
   DecideArgs dec;         // residual launches: fused sum + decision (last block)
 };
 size_t tile_lds_bytes(int TX, int RY, int K);
-bool tile_config_ok(int TX, int RY, int K);
+// a lane owns up to kTileMaxSweeps region rows (kept in registers across the launch's levels)
+constexpr int kTileMaxSweeps = 8;
+bool tile_config_ok(int TX, int RY, int K, int CPL = 4, int NT = 256);
 int tile_count(int NX, int NY, int TX, int TY);
 void launch_tile(TileArgs a, int precision, bool residual, hipStream_t s);
 // No-op launches of every tiled-kernel variant of `precision`: HIP loads a translation unit's

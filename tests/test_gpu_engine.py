@@ -226,13 +226,20 @@ TILE_SIZES = [(1, 1), (3, 2), (80, 64), (97, 131), (160, 128), (257, 509), (320,
 
 @pytest.mark.parametrize("nx,ny", TILE_SIZES)
 @pytest.mark.parametrize("boundary", [0, 1])
-@pytest.mark.parametrize("width,K", [(64, 8), (128, 16), (64, 1), (128, 5)])
-def test_tiled_bitexact(native, gpu, nx, ny, boundary, width, K):
+@pytest.mark.parametrize("width,K", [(64, 8), (128, 16), (64, 1), (128, 5), (32, 6), (32, 14)])
+@pytest.mark.parametrize("nt,cpl", [(256, 4), (1024, 4), (1024, 2), (256, 1)])
+def test_tiled_bitexact(native, gpu, nx, ny, boundary, width, K, nt, cpl):
     steps = 2 * K + 5  # full chunks and a partial one
-    eng = native.Engine(nx, ny, boundary=boundary, device=gpu, small_grid_lds=False, tiled=1, tile_width=width,
-                        tile_k=K, tile_rows=16, poison=True)
+    kw = dict(boundary=boundary, device=gpu, small_grid_lds=False, tiled=1, tile_width=width, tile_k=K, tile_rows=16,
+              tile_threads=nt, tile_cpl=cpl, poison=True)
+    if 16 + 2 * K > 8 * nt // (width // max(cpl, width // 64)):  # a lane owns at most 8 region rows
+        with pytest.raises(Exception, match="tile configuration"):
+            native.Engine(nx, ny, **kw)
+        return
+    eng = native.Engine(nx, ny, **kw)
     st = eng.run(steps)
     assert st["path"] == "tiled" and st["steps_done"] == steps and eng.tile_config() == [16, width, K]
+    assert eng.tile_threads() == nt and eng.tile_cpl() == max(cpl, width // 64)
     ref = oracle(native, nx, ny, steps, boundary)["grid"]
     got = eng.download(0)
     assert np.array_equal(got, ref), np.abs(got - ref).max()
@@ -240,20 +247,23 @@ def test_tiled_bitexact(native, gpu, nx, ny, boundary, width, K):
 
 @pytest.mark.parametrize("per", [(True, False), (False, True), (True, True)])
 @pytest.mark.parametrize("boundary", [0, 1])
-def test_tiled_periodic(native, gpu, per, boundary):
+@pytest.mark.parametrize("nt,cpl,width", [(256, 4, 64), (1024, 4, 64), (1024, 1, 32), (1024, 2, 64)])
+def test_tiled_periodic(native, gpu, per, boundary, nt, cpl, width):
     nx, ny, steps = 45, 70, 29
     eng = native.Engine(nx, ny, boundary=boundary, periodic_x=per[0], periodic_y=per[1], device=gpu, tiled=1,
-                        tile_k=6, tile_rows=8)
+                        tile_k=6, tile_rows=8, tile_threads=nt, tile_cpl=cpl, tile_width=width)
     assert eng.run(steps)["path"] == "tiled"
     assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps, boundary, per=per)["grid"])
 
 
 @pytest.mark.parametrize("precision", [0, 1])
-def test_tiled_convergence_and_fp32(native, gpu, precision):
+@pytest.mark.parametrize("nt,cpl", [(256, 4), (1024, 4), (1024, 2), (1024, 1)])
+def test_tiled_convergence_and_fp32(native, gpu, precision, nt, cpl):
     nx, ny = 120, 200
     kw = dict(convergence=True, interval=7, sensitivity=5e3)
     ref = oracle(native, nx, ny, 3000, 0, precision=precision, **kw)
-    eng = native.Engine(nx, ny, precision=precision, device=gpu, tiled=1, tile_k=8, small_grid_lds=False, **kw)
+    eng = native.Engine(nx, ny, precision=precision, device=gpu, tiled=1, tile_k=8, tile_threads=nt, tile_cpl=cpl,
+                        small_grid_lds=False, **kw)
     st = eng.run(3000)
     assert st["path"] == "tiled"
     assert st["steps_done"] == ref["steps_done"] and st["converged"] == ref["converged"]

@@ -1,5 +1,5 @@
 """Small/medium-grid path sweep on one GPU: the whole-grid LDS solver, the streaming kernel
-and LDS-tiled configurations (width RY, steps per launch K, tile rows TX), at the reference's
+and LDS-tiled configurations (width RY, steps per launch K, tile rows TX, workgroup size NT, cells per lane CPL), at the reference's
 published grid sizes (Report.pdf p.21/p.26).  Prints us/step (best of 3, device time).
 
   python tools/tile_sweep.py [--steps 1000] [--sizes 80x64,160x128,...] [--precision ref|fp32]
@@ -33,19 +33,23 @@ for size in a.sizes.split(","):
         rows.append(("lds", best_us(n.Engine(nx, ny, precision=prec, device=0, tiled=0), a.steps)))
     rows.append(("stream K8", best_us(n.Engine(nx, ny, precision=prec, device=0, tiled=0, small_grid_lds=False), a.steps)))
     auto = n.Engine(nx, ny, precision=prec, device=0)
-    rows.append((f"auto {auto.tile_config() if auto.tiled() else ''}", best_us(auto, a.steps)))
-    widths = (64, 128)
-    ks = (4, 8, 16) if not a.quick else (8, 16)
-    txs = (8, 16, 32, 64) if not a.quick else (16, 32)
+    rows.append((f"auto {auto.tile_config() + [auto.tile_threads(), auto.tile_cpl()] if auto.tiled() else ''}", best_us(auto, a.steps)))
+    widths = (32, 64, 128)
+    ks = (4, 8, 12, 16) if not a.quick else (6, 8, 12, 16)
+    txs = (4, 8, 16, 32, 64) if not a.quick else (4, 8, 16, 32)
     for w in widths:
         for K in ks:
             for tx in txs:
-                try:
-                    e = n.Engine(nx, ny, precision=prec, device=0, tiled=1, tile_width=w, tile_k=K, tile_rows=tx,
-                                 small_grid_lds=False)
-                except Exception:
-                    continue
-                rows.append((f"tiled RY={w:3d} K={K:2d} TX={tx:2d}", best_us(e, a.steps)))
+                for nt in ((256, 1024) if not a.quick else (1024,)):
+                    for cpl in (1, 2, 4):
+                        if w // cpl > 64:
+                            continue
+                        try:
+                            e = n.Engine(nx, ny, precision=prec, device=0, tiled=1, tile_width=w, tile_k=K,
+                                         tile_rows=tx, tile_threads=nt, tile_cpl=cpl, small_grid_lds=False)
+                        except Exception:
+                            continue
+                        rows.append((f"tiled RY={w:3d} K={K:2d} TX={tx:2d} NT={nt:4d} CPL={cpl}", best_us(e, a.steps)))
     rows.sort(key=lambda r: r[1])
     print(f"== {nx}x{ny} ({a.precision}, {a.steps} steps): best {rows[0][0]} {rows[0][1]:.3f} us/step", flush=True)
     for name, us in rows[:8]:
