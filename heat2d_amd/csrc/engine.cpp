@@ -585,6 +585,10 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   a.per_y = opt_.periodic_y;
   a.partials = tl.partials;
   a.dummy = d_dummy_;
+  // write-through stores address rows by 32-bit offsets from a unit's base: tiles whose storage
+  // spans 2^31 bytes or more (HBM-filling ones) keep plain stores
+  a.wt = (opt_.wt_store < 0 ? 1 : opt_.wt_store) != 0 &&
+         (double)(g.xcell + 2 * g.G) * (double)g.pitch * sizeof(float) < 2147483648.0 - 1048576.0;
   const bool whole = which == 0 || which == 3;  // the launch covers every unit of the tile
   // A lone single-process tile sums its partials and decides in ONE small kernel behind the
   // launch (device_decide).  (A last-wave in-kernel reduction was measured slower here: 1024

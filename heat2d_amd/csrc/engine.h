@@ -91,6 +91,8 @@ struct EngineOptions {
   int fused_check = -1;
   int direct_release = -1;
   int direct_acquire = -1;
+  // Streaming kernel output rows: 0 plain stores, 1 write-through (sc1), -1 the measured default.
+  int wt_store = -1;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
   bool poison = false;        // debug canary: NaN in every cell no valid update may read

@@ -133,6 +133,10 @@ struct StreamArgs {
   DecideArgs dec;  // residual launches of a single-tile run: fused sum + decision
   int rel = 0;  // signal release: 0 system scope, 1 agent scope, 2 drain only (payload in uncached memory)
   int acq = 0;  // halo-wait acquire: 0 system scope, 1 agent scope, 2 compiler ordering only
+  // Output row stores: 0 plain (write-back L2), 1 write-through (buffer_store sc1: the line
+  // leaves the XCD's L2 at once, so the launch ends with no dirty L2 to write back — the
+  // dependent kernel boundary then costs the bare ~1.7 us instead of + dirty bytes / 6 TB/s).
+  int wt = 0;
   long long halo_polls = 0;
   unsigned int* timed_out = nullptr;
   unsigned int* timed_out_host = nullptr;  // host-mapped mirror of *timed_out (polled by the host per chunk)

@@ -118,7 +118,25 @@ struct LaneCtx {
   float* kout;     // RESID launches: level K-1 value of each output cell (rollback state) or a dummy
   int64_t kpitch;  // row pitch of kout (0 for the dummy slot)
   bool st0, st1, st2, st3;  // element is an owned output cell (residual accounting)
+  // write-through path (StreamArgs::wt): wave-uniform base = the unit's lowest-address output
+  // row, the byte offset of output row orow = obo + orow * obs (reverse units: negative step),
+  // and this lane's byte offset in a row (out-of-range lanes: >= 2^31, past num_records, so the
+  // buffer store drops them — no dummy slot).  The host keeps every offset below 2^31.
+  float* obase;
+  int obo, obs;
+  unsigned voff;
 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Store one lane's float4 of an output row write-through (buffer_store_dwordx4 ... sc1):
+// 16-B sc1 stores cost about a plain store, and leave no dirty line in the L2.  The resource is
+// loop-invariant (the unit's base); the row moves through the scalar offset.
+__device__ __forceinline__ void store_row_wt(float* base, unsigned voff, int soff, const float4& o) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  const u32x4 d = {__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(o.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)voff, soff, 16 /* sc1 */);
+}
 
 __device__ __forceinline__ double sq_diff(float a, float b) {
   const double d = (double)a - (double)b;
@@ -166,7 +184,7 @@ __device__ __forceinline__ float4 apply_edge(float4 o, const float4& C, int64_t 
 // Process stream input row `ir` (level-0 value `cur`) through levels 1..TMAX (TMAX <= K).
 // Slot parity P = ir & 1: S[l][P] holds level-l row (ir-l-2), S[l][1-P] holds row (ir-l-1).
 // Level t computes row (ir - t) of level t.  Level K writes output row ir - 2K (unit-relative).
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, int P, int TMAX>
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, int P, int TMAX>
 __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int ir, const LaneCtx& c, const Coef& k,
                                             double& racc) {
 #pragma unroll
@@ -182,7 +200,8 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
     S[t - 1][P] = cur;
     if (t == K) {
       const int64_t orow = ir - 2 * K;
-      *reinterpret_cast<float4*>(c.sout + orow * c.spitch) = o;
+      if constexpr (WT) store_row_wt(c.obase, c.voff, c.obo + (int)orow * c.obs, o);
+      else *reinterpret_cast<float4*>(c.sout + orow * c.spitch) = o;
       if (orow < c.prows) *reinterpret_cast<float4*>(c.pout + orow * c.ppitch) = o;  // uniform branch
       if constexpr (RESID) {
         *reinterpret_cast<float4*>(c.kout + orow * c.kpitch) = mid;
@@ -199,14 +218,14 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
 // Prologue row IR (compile-time): levels t <= IR/2 are primed.
 // Stream rows [0, K) are the unit's outer cone rows: for a halo unit, the ghost rows, read from
 // hrowp (the halo receive buffer of the direct pipeline; == rowp otherwise).
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, int IR>
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, int IR>
 __device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4* __restrict__ rowp,
                                          const float4* __restrict__ hrowp, int64_t pitch4, const LaneCtx& c,
                                          const Coef& k, double& racc) {
   if constexpr (IR < 2 * K) {
     const float4 v = (IR < K ? hrowp : rowp)[(int64_t)IR * pitch4];
-    process_row<K, F32, EDGE, FIXED, RESID, IR & 1, IR / 2>(S, v, IR, c, k, racc);
-    prologue<K, F32, EDGE, FIXED, RESID, IR + 1>(S, rowp, hrowp, pitch4, c, k, racc);
+    process_row<K, F32, EDGE, FIXED, RESID, WT, IR & 1, IR / 2>(S, v, IR, c, k, racc);
+    prologue<K, F32, EDGE, FIXED, RESID, WT, IR + 1>(S, rowp, hrowp, pitch4, c, k, racc);
   }
 }
 
@@ -228,7 +247,7 @@ __device__ __forceinline__ void unit_signal(unsigned long long* sig, int lane, i
 
 // sig_at > 0: signal (once) before processing stream row sig_at (a multiple of 4 past 2K),
 // i.e. once every output row < sig_at - 2K is stored.
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID>
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT>
 __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const float4* __restrict__ hrowp,
                                          int64_t pitch4, int n, const LaneCtx& c, const Coef& k, double& racc,
                                          int sig_at, unsigned long long* sig, int lane) {
@@ -242,14 +261,14 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
   float4 pf[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(2 * K + d, n - 1) * pitch4];
-  prologue<K, F32, EDGE, FIXED, RESID, 0>(S, rowp, hrowp, pitch4, c, k, racc);
+  prologue<K, F32, EDGE, FIXED, RESID, WT, 0>(S, rowp, hrowp, pitch4, c, k, racc);
 
   int ir0 = 2 * K;  // even: slot parity of sub-step d is d & 1
 #define H2D_STEADY(D)                                                        \
   {                                                                          \
     const float4 nw = pf[D];                                                 \
     pf[D] = rowp[(int64_t)min(ir0 + (D) + 4, n - 1) * pitch4];               \
-    process_row<K, F32, EDGE, FIXED, RESID, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
+    process_row<K, F32, EDGE, FIXED, RESID, WT, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
   for (; ir0 + 4 <= n; ir0 += 4) {
     if (ir0 == sig_at) unit_signal(sig, lane, c.rel);
@@ -260,9 +279,9 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
   }
 #undef H2D_STEADY
   // tail: at most 3 rows
-  if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, 0, K>(S, pf[0], ir0, c, k, racc);
-  if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
-  if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
+  if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, 0, K>(S, pf[0], ir0, c, k, racc);
+  if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
+  if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
   // the loop visits every sig_at candidate below its exit value: a signal point at or past the
   // exit has not fired yet (unit shorter than its signal rows, or kUnitSigEnd)
   if (sig_at >= ir0) unit_signal(sig, lane, c.rel);
@@ -282,12 +301,12 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-template <int K, bool F32, bool RESID, int EDGE>
+template <int K, bool F32, bool RESID, bool WT, int EDGE>
 __device__ __forceinline__ void run_edge(const float4* rowp, const float4* hrowp, int64_t pitch4, int n,
                                          const LaneCtx& c, const Coef& k, double& racc, bool fixed, int sig_at,
                                          unsigned long long* sig, int lane) {
-  if (fixed) run_unit<K, F32, EDGE, true, RESID>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
-  else run_unit<K, F32, EDGE, false, RESID>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+  if (fixed) run_unit<K, F32, EDGE, true, RESID, WT>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+  else run_unit<K, F32, EDGE, false, RESID, WT>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
 }
 
 // The decision of a convergence check, by the one lane that holds the total.
@@ -327,7 +346,7 @@ __device__ __forceinline__ void publish_partial(double* partials, int slot, doub
   }
 }
 
-template <int K, bool F32, bool RESID>
+template <int K, bool F32, bool RESID, bool WT>
 __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int w = (int)blockIdx.x * 4 + wv;
@@ -390,6 +409,10 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   float* out = a.dst + (a.G + xout) * a.pitch + a.PL + cb;
   c.sout = in_out ? out : a.dummy + 4 * lane;
   c.spitch = in_out ? (rev ? -a.pitch : a.pitch) : 0;
+  c.obase = a.dst + (a.G + x0) * a.pitch + a.PL + u.cb;
+  c.obs = (int)((rev ? -a.pitch : a.pitch) * (int64_t)sizeof(float));
+  c.obo = rev ? (h - 1) * (int)(a.pitch * (int64_t)sizeof(float)) : 0;
+  c.voff = in_out ? 16u * (unsigned)lane : 0x80000000u;
   c.st0 = in_out;
   c.st1 = in_out && cb + 1 < a.ycell;
   c.st2 = in_out && cb + 2 < a.ycell;
@@ -417,10 +440,10 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
                      : ((u.flags & kUnitSigEnd) != 0 || a.sig_rows <= 0) ? (1 << 30)
                                                                           : 2 * K + ((a.sig_rows + 3) & ~3);
   switch (u.flags & 3) {
-    case 0: run_unit<K, F32, 0, false, RESID>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane); break;
-    case 1: run_edge<K, F32, RESID, 1>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
-    case 2: run_edge<K, F32, RESID, 2>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
-    default: run_edge<K, F32, RESID, 3>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+    case 0: run_unit<K, F32, 0, false, RESID, WT>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane); break;
+    case 1: run_edge<K, F32, RESID, WT, 1>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+    case 2: run_edge<K, F32, RESID, WT, 2>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+    default: run_edge<K, F32, RESID, WT, 3>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
   }
   if constexpr (RESID) {
     racc = wave_sum(racc);
@@ -432,20 +455,22 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
 
 }  // namespace
 
+template <int K, bool WT>
+auto stream_fn(bool f32, bool resid) -> void (*)(StreamArgs) {
+  if (f32) return resid ? stream_kernel<K, true, true, WT> : stream_kernel<K, true, false, WT>;
+  return resid ? stream_kernel<K, false, true, WT> : stream_kernel<K, false, false, WT>;
+}
+
 template <int K>
 void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s) {
   const int blocks = std::max(1, (a.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_kernels)
-  void (*fn)(StreamArgs);
-  if (f32) fn = resid ? stream_kernel<K, true, true> : stream_kernel<K, true, false>;
-  else fn = resid ? stream_kernel<K, false, true> : stream_kernel<K, false, false>;
+  void (*fn)(StreamArgs) = a.wt ? stream_fn<K, true>(f32, resid) : stream_fn<K, false>(f32, resid);
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, a);
 }
 
 template <int K>
 int stream_blocks_per_cu(bool f32, bool resid) {
-  void (*fn)(StreamArgs);
-  if (f32) fn = resid ? stream_kernel<K, true, true> : stream_kernel<K, true, false>;
-  else fn = resid ? stream_kernel<K, false, true> : stream_kernel<K, false, false>;
+  void (*fn)(StreamArgs) = stream_fn<K, false>(f32, resid);
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), 256, 0) != hipSuccess) return 1;
   return nb > 0 ? nb : 1;

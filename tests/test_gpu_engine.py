@@ -305,6 +305,24 @@ def test_ipc_direct_self_exchange_row_periodic(native, gpu, nx, ny, boundary, tb
     assert np.array_equal(eng.download(0), ref)
 
 
+@pytest.mark.parametrize("wt", [0, 1])
+@pytest.mark.parametrize("path", ["single", "tiles", "ipc"])
+def test_output_store_policy_bitexact(native, gpu, wt, path):
+    """Plain and write-through (buffer_store sc1, scalar row offsets incl. bottom-up units)
+    output stores give the same grid as the oracle on every streaming path."""
+    nx, ny, steps, boundary = 300, 701, 29, 1
+    kw = dict(boundary=boundary, tblock=8, device=gpu, poison=True, wt_store=wt, small_grid_lds=False, tiled=0)
+    if path == "ipc":
+        eng = _ipc_engine(native, nx=nx, ny=ny, periodic_x=True, **kw)
+        per = (True, False)
+    else:
+        eng = native.Engine(nx, ny, gridx=3 if path == "tiles" else 1, **kw)
+        per = (False, False)
+    eng.run(steps)
+    got = eng.download(0) if path != "tiles" else _gather(eng, nx, ny)
+    assert np.array_equal(got, oracle(native, nx, ny, steps, boundary, per=per)["grid"])
+
+
 def test_ipc_direct_convergence_and_reprime(native, gpu):
     nx, ny = 96, 300
     kw = dict(convergence=True, interval=10, sensitivity=1e12)

@@ -16,6 +16,9 @@ side = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 960
 Ks = [int(k) for k in sys.argv[3].split(",")] if len(sys.argv) > 3 else [4, 6, 8, 10, 12, 16]
 cap = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # wave_capacity override (0: occupancy query)
+# extra engine options, "name=value,name=value" (e.g. wt_store=0)
+opts = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in sys.argv[5].split(",")} if len(sys.argv) > 5 else {}
+Ns = [int(v) for v in sys.argv[6].split(",")] if len(sys.argv) > 6 else [1, 2, 4, 8, 16]
 
 
 def timed(e, steps, reps=3):
@@ -31,10 +34,10 @@ def timed(e, steps, reps=3):
 
 
 t1 = None
-for N in (1, 2, 4, 8, 16):
+for N in Ns:
     rows = side // N
     for K in Ks:
-        plain = n.Engine(rows, side, tblock=K, device=0, small_grid_lds=False, tiled=0, wave_capacity=cap)
+        plain = n.Engine(rows, side, tblock=K, device=0, small_grid_lds=False, tiled=0, wave_capacity=cap, **opts)
         up = timed(plain, steps)
         del plain
         if N == 1:
@@ -44,7 +47,7 @@ for N in (1, 2, 4, 8, 16):
             continue
         try:
             e = n.Engine(rows, side, periodic_x=True, tblock=K, device=0, ranks=[0], transport=n.TRANSPORT_IPC,
-                         halo_timeout_s=5.0, wave_capacity=cap)
+                         halo_timeout_s=5.0, wave_capacity=cap, **opts)
             e.ipc_open([e.ipc_handle()])
             e.ipc_prime()
             ud = timed(e, steps)
