@@ -151,6 +151,8 @@ def main() -> int:
         # device-level alignment (RCCL all-reduce) when every rank has its own GPU
         if on_gpu and not ctx.device_barrier(device):
             sync()
+        # host-level alignment: node-local spin barrier (exit skew ~1 us instead of gloo's tens)
+        ctx.node_barrier()
 
     # ---- pre-warm (untimed, time-based, collectively agreed count) + W warm-up steps --------
     # The pre-warm replays the timed run's exact shape (runs of K steps: the same chunk depths,

@@ -24,10 +24,48 @@
 #include "decomposition.h"
 #include "engine.h"
 #include "io.h"
+#include "shm_barrier.h"
+
+#include <memory>
+#include <random>
 
 using namespace h2d;
 
 namespace {
+
+// Node-local spin barrier for the timed region (shm_barrier.h), set up collectively: rank 0
+// creates a uniquely named segment, the others open it, and every rank keeps it only if all
+// succeeded (ranks on another node cannot open it: then everyone uses the TCP barrier alone).
+// The name is unlinked as soon as all ranks hold the mapping.
+std::unique_ptr<ShmBarrier> node_barrier(Bootstrap& boot) {
+  if (boot.world() <= 1) return nullptr;
+  std::string name;
+  if (boot.rank() == 0) {
+    std::random_device rd;
+    name = "/heat2d_bar_" + std::to_string(getpid()) + "_" + std::to_string(rd());
+  }
+  name = boot.broadcast(name);
+  std::unique_ptr<ShmBarrier> b;
+  if (boot.rank() == 0) {
+    try {
+      b = std::make_unique<ShmBarrier>(name, 0, boot.world(), true);
+    } catch (const std::exception&) {
+      b.reset();
+    }
+  }
+  boot.barrier();  // the segment exists before anyone opens it
+  if (boot.rank() != 0) {
+    try {
+      b = std::make_unique<ShmBarrier>(name, boot.rank(), boot.world(), false);
+    } catch (const std::exception&) {
+      b.reset();
+    }
+  }
+  const bool all = boot.allreduce_min(b ? 1.0 : 0.0) > 0.5;
+  if (b) b->unlink();  // rank 0: every rank has opened (or given up on) the name by now
+  if (!all) b.reset();
+  return b;
+}
 
 struct Preset {
   int64_t nx, ny, steps;
@@ -281,6 +319,7 @@ int main(int argc, char** argv) {
 
   try {
     Bootstrap boot(env.rank, world, env.addr, env.port);
+    std::unique_ptr<ShmBarrier> shm = node_barrier(boot);
     Engine e(o);
     if (o.transport == kTransportIpc && e.has_exchange()) {
       e.ipc_open(boot.allgather(e.ipc_handle()));
@@ -330,6 +369,7 @@ int main(int argc, char** argv) {
     std::fflush(stdout);
     e.synchronize();
     boot.barrier();
+    if (shm) shm->wait();  // node-local ranks leave within ~1 us of each other (shm_barrier.h)
     const auto t0 = std::chrono::steady_clock::now();
     const RunStats st = o.transport == kTransportExternal && e.has_exchange() ? run_external(e, boot, steps, o.sensitivity)
                                                                              : e.run(steps);

@@ -277,8 +277,8 @@ class Solver:
 
     def run(self, steps: Optional[int] = None) -> RunResult:
         steps = self.cfg.steps if steps is None else steps
-        self.ctx.barrier()
         self.engine.synchronize()
+        self.ctx.node_barrier()  # gloo barrier + node-local spin: ranks start within ~1 us
         t0 = time.perf_counter()
         st = self.run_steps(steps)
         self.engine.synchronize()
