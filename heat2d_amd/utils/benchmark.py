@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -174,10 +175,15 @@ def run_gate(ctx, make_solver: Callable[[str, str, int, int, int], object], orac
 
     nx, ny, steps = gate_grid(ctx.world, gx, gy, G)
     tried = []
+    # test hook: HEAT2D_GATE_FAIL="ipc,rccl" makes those transports fail the gate (rehearses
+    # the downgrade path on hardware where they would pass)
+    forced = {t for t in os.environ.get("HEAT2D_GATE_FAIL", "").split(",") if t}
     for transport, pipeline in cands:
         ok, why = 1, ""
         s = None
         try:
+            if transport in forced:
+                raise RuntimeError("failure injected by HEAT2D_GATE_FAIL")
             s = make_solver(transport, pipeline, nx, ny, steps)
             s.run_steps(steps)
             s.engine.synchronize()

@@ -134,3 +134,21 @@ def test_bench_weak_and_blocks_cpu_rehearsal(tmp_path):
     assert d["scaling"] == "weak" and d["config"]["grid"] == [80, 80] and d["config"]["grid_per_gpu"] == [40, 40]
     assert d["config"]["parallelism"] == "blocks2x2" and d["verified"] is None
     assert abs(d["speedup"] - 4 * d["efficiency"]) < 1e-12
+
+
+def test_bench_gate_all_candidates_fail_cpu(tmp_path):
+    """Every transport fails the gate: rank 0 prints an error record naming what was tried and
+    the job exits non-zero instead of timing an unverified configuration."""
+    env = dict(os.environ, HEAT2D_NO_BUILD="1", HEAT2D_GATE_FAIL="torch")
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "4", "--warmup", "1", "--side", "32", "--device", "cpu"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    import json
+
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["error"] == "no transport passed the correctness gate"
+    assert rec["gate"][0]["transport"] == "torch" and not rec["gate"][0]["ok"]
+    assert "HEAT2D_GATE_FAIL" in rec["gate"][0]["detail"]

@@ -76,6 +76,18 @@ def test_gpu_bench_two_ranks_ipc(tmp_path):
     assert d["gate"][0]["ok"] and d["verified"] is True
 
 
+def test_gpu_bench_two_ranks_gate_downgrade(tmp_path, monkeypatch):
+    """The first candidate (direct IPC) fails the gate (injected): every rank falls back to the
+    next one together, the run is timed with it and the JSON says what failed."""
+    monkeypatch.setenv("HEAT2D_GATE_FAIL", "ipc")
+    out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5", "--side",
+                        "512", "--prewarm-s", "0"], str(tmp_path))
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert d["gate"][0]["transport"] == "ipc" and not d["gate"][0]["ok"]
+    assert d["gate"][1]["ok"] and d["config"]["transport"] == d["gate"][1]["transport"] == "host"
+    assert d["verified"] is True
+
+
 def test_gpu_bench_two_ranks_host_transport(tmp_path):
     """Two ranks on the one GPU: the gate, the strong-scaling default and the in-job
     single-GPU reference with bit-exact verification of the timed run."""
