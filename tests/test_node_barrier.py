@@ -43,3 +43,23 @@ def test_shm_barrier_single_process(native):
         assert b.wait(1.0) >= 0.0
     b.unlink()
     assert f"heat2d_bar_test_{os.getpid()}" not in _segments()
+
+
+def test_shm_barrier_rejects_bad_arguments(native):
+    import pytest
+
+    name = f"/heat2d_bar_args_{os.getpid()}"
+    with pytest.raises(Exception):
+        native.ShmBarrier("no_leading_slash", 0, 2, True)
+    with pytest.raises(Exception):
+        native.ShmBarrier(name, 2, 2, True)  # rank out of range
+    owner = native.ShmBarrier(name, 0, 2, True)
+    with pytest.raises(Exception):
+        native.ShmBarrier(name, 1, 3, False)  # world size differs from the creator's
+    with pytest.raises(Exception):
+        native.ShmBarrier(name, 0, 2, True)  # exclusive create: the name exists
+    with pytest.raises(Exception):
+        owner.wait(0.05)  # rank 1 never arrives: bounded wait
+    owner.unlink()
+    with pytest.raises(Exception):
+        native.ShmBarrier(name, 1, 2, False)  # unlinked: nothing to open
