@@ -5,7 +5,10 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 by ``torch.distributed.run`` with one rank per GPU.  A "step" is one Jacobi time step of the
 whole grid.  W untimed warm-up steps, then EXACTLY K timed steps bracketed by a barrier and
 ``torch.cuda.synchronize()`` on both sides; the max over ranks is reported by rank 0 as one
-JSON line.  ``value`` is the whole-job throughput (all GPUs).
+JSON line.  ``value`` is the whole-job throughput (all GPUs).  The timed run is repeated
+(``--repeat``, default 3, each exactly K steps behind its own barrier) and the MEDIAN is
+reported, every repetition listed in ``repeats_s``: a 20-step run lasts ~170 µs on one GPU, so
+a single host hiccup would otherwise decide the number (one such run took 236 µs).
 
 Default configuration (``--config 4096-strong``, the BASELINE metric): ONE 4096×4096 fp32 grid
 split over the N GPUs (strong scaling; 1-D row strips, the layout whose halos are contiguous
@@ -63,7 +66,9 @@ def main() -> int:
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-gate", action="store_true", help="skip the pre-timing correctness gate (N > 1)")
     ap.add_argument("--no-reference", action="store_true", help="skip the in-job single-GPU reference run")
-    ap.add_argument("--repeat", type=int, default=1, help="timed repetitions (best reported)")
+    ap.add_argument("--repeat", type=int, default=3,
+                    help="timed runs of exactly --steps steps each; the MEDIAN is reported (a 20-step run lasts "
+                         "~170 us, so one host hiccup would otherwise decide the number), all are in repeats_s")
     ap.add_argument("--prewarm-s", type=float, default=0.3,
                     help="seconds of untimed stencil work before the warm-up steps, so the GPU reaches its "
                          "steady power state (the first ~10 ms after idle run at lower clocks)")
@@ -175,7 +180,7 @@ def main() -> int:
         run(a.warmup)
 
     # ---- timed region -----------------------------------------------------------------------
-    best, res, times = None, None, []
+    res, times = None, []
     for _ in range(max(1, a.repeat)):
         sync_barrier()
         t0 = time.perf_counter()
@@ -183,7 +188,7 @@ def main() -> int:
         sync()
         dt = ctx.allreduce_max(time.perf_counter() - t0)
         times.append(dt)
-        best = dt if best is None else min(best, dt)
+    best = sorted(times)[(len(times) - 1) // 2]  # median (lower median for an even count)
     total_steps = prewarm_steps + max(0, a.warmup) + a.steps * max(1, a.repeat)
     if res["steps_done"] != total_steps:
         raise SystemExit(f"bench: step accounting error ({res['steps_done']} != {total_steps})")
@@ -221,7 +226,7 @@ def main() -> int:
                 e.run(a.steps)
                 e.synchronize()
                 ts.append(time.perf_counter() - t0)
-            t1 = min(ts)
+            t1 = sorted(ts)[(len(ts) - 1) // 2]
             if scaling == "strong":
                 full = e.download(0)
                 verified = all(B.digest_of_region(full, k) == v for d in digests for k, v in d.items())
@@ -262,6 +267,7 @@ def main() -> int:
             "data": "synthetic center-hot initial field (exact formula, generated on device)",
             "elapsed_s": best,
             "repeats_s": times,
+            "timing": f"median of {len(times)} timed runs of exactly {a.steps} steps (max over ranks each)",
             "prewarm_steps": prewarm_steps,
             "gate": (gate.tried if gate is not None else None),
             "config": {

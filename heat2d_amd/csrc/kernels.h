@@ -185,8 +185,10 @@ void launch_lds_solver(const float* in, int64_t in_pitch, float* out, int64_t ou
 }  // namespace h2d
 
 namespace h2d {
-template <int K>
-void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s);
-template <int K>
-int stream_blocks_per_cu(bool f32, bool resid);
+// per-variant launch / occupancy of the streaming kernel (stream_kernel.hpp; instantiated in
+// generated TUs, one per (K, precision, residual))
+template <int K, bool F32, bool RESID>
+void launch_stream_kv(const StreamArgs& a, hipStream_t s);
+template <int K, bool F32, bool RESID>
+int stream_blocks_per_cu_v();
 }  // namespace h2d

@@ -1,6 +1,6 @@
 // heat2d_amd — auxiliary HIP kernels (init, halo copies, reductions, naive step, the
 // small-grid LDS-resident solver) and the streaming-kernel dispatch.  The streaming stencil
-// itself lives in stream_kernel.hpp, instantiated once per K in stream_k*.hip.
+// itself lives in stream_kernel.hpp, instantiated per (K, precision, residual) in generated TUs.
 // Compiled with -ffp-contract=off.
 #include "stream_kernel.hpp"
 
@@ -273,12 +273,33 @@ __global__ __launch_bounds__(1024) void lds_solver_kernel(const float* __restric
 }  // namespace
 
 #define H2D_K_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(12) X(16)
-#define H2D_EXTERN(K) extern template void launch_stream_k<K>(const StreamArgs&, bool, bool, hipStream_t);
+// The variants live in generated translation units (heat2d_amd/_build.py: K_LIST there must
+// match this list).
+#define H2D_EXTERN(K)                                                                          \
+  extern template void launch_stream_kv<K, false, false>(const StreamArgs&, hipStream_t);      \
+  extern template void launch_stream_kv<K, false, true>(const StreamArgs&, hipStream_t);       \
+  extern template void launch_stream_kv<K, true, false>(const StreamArgs&, hipStream_t);       \
+  extern template void launch_stream_kv<K, true, true>(const StreamArgs&, hipStream_t);        \
+  extern template int stream_blocks_per_cu_v<K, false, false>();                                \
+  extern template int stream_blocks_per_cu_v<K, true, false>();
 H2D_K_LIST(H2D_EXTERN)
 #undef H2D_EXTERN
-#define H2D_EXTERN2(K) extern template int stream_blocks_per_cu<K>(bool, bool);
-H2D_K_LIST(H2D_EXTERN2)
-#undef H2D_EXTERN2
+
+template <int K>
+void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s) {
+  if (f32) {
+    if (resid) launch_stream_kv<K, true, true>(a, s);
+    else launch_stream_kv<K, true, false>(a, s);
+  } else {
+    if (resid) launch_stream_kv<K, false, true>(a, s);
+    else launch_stream_kv<K, false, false>(a, s);
+  }
+}
+
+template <int K>
+int stream_blocks_per_cu(bool f32, bool /*resid*/) {
+  return f32 ? stream_blocks_per_cu_v<K, true, false>() : stream_blocks_per_cu_v<K, false, false>();
+}
 
 int64_t stream_wave_capacity(int K, int precision, int device) {
   // The ref-precision stencil is VALU-bound (about 11 fp64-rate VALU ops per cell-step, one

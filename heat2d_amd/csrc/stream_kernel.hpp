@@ -25,7 +25,8 @@
 // one fp64 op less (10 fp64-rate ops per cell).  No MFMA: a 5-point stencil has no
 // dot-product of depth >= 16 and the contract forbids the contraction it would impose.
 //
-// Included by the per-K translation units stream_k*.hip (compiled in parallel); every TU is
+// Included by the generated per-variant translation units (build/gen/stream_k*.hip, compiled in
+// parallel); every TU is
 // compiled with -ffp-contract=off.
 #pragma once
 #include "kernels.h"
@@ -455,22 +456,19 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
 
 }  // namespace
 
-template <int K, bool WT>
-auto stream_fn(bool f32, bool resid) -> void (*)(StreamArgs) {
-  if (f32) return resid ? stream_kernel<K, true, true, WT> : stream_kernel<K, true, false, WT>;
-  return resid ? stream_kernel<K, false, true, WT> : stream_kernel<K, false, false, WT>;
-}
-
-template <int K>
-void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s) {
+// One (K, precision, residual) variant of the launch, both store flavours.  Each variant is
+// instantiated in its own generated translation unit (heat2d_amd/_build.py writes
+// build/gen/stream_k<K>_f<F32>r<RESID>.hip), so the 44 stencil objects compile in parallel.
+template <int K, bool F32, bool RESID>
+void launch_stream_kv(const StreamArgs& a, hipStream_t s) {
   const int blocks = std::max(1, (a.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_kernels)
-  void (*fn)(StreamArgs) = a.wt ? stream_fn<K, true>(f32, resid) : stream_fn<K, false>(f32, resid);
+  void (*fn)(StreamArgs) = a.wt ? stream_kernel<K, F32, RESID, true> : stream_kernel<K, F32, RESID, false>;
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, a);
 }
 
-template <int K>
-int stream_blocks_per_cu(bool f32, bool resid) {
-  void (*fn)(StreamArgs) = stream_fn<K, false>(f32, resid);
+template <int K, bool F32, bool RESID>
+int stream_blocks_per_cu_v() {
+  void (*fn)(StreamArgs) = stream_kernel<K, F32, RESID, false>;
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), 256, 0) != hipSuccess) return 1;
   return nb > 0 ? nb : 1;
