@@ -33,7 +33,12 @@ def torchrun(n, args, cwd, timeout=300):
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env["OMP_NUM_THREADS"] = "1"
     env["HEAT2D_NO_BUILD"] = "1"
-    r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    for _attempt in range(3):  # retry only a launcher port collision, with a fresh port
+        r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0 and "EADDRINUSE" in r.stderr:
+            cmd[cmd.index("--master-port") + 1] = str(free_port())
+            continue
+        break
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
 
@@ -97,7 +102,12 @@ def _bench(n, args, cwd):
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
                "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), *args]
-    r = subprocess.run(cmd, cwd=str(cwd), env=env, capture_output=True, text=True, timeout=300)
+    for _attempt in range(3):  # retry only a launcher port collision, with a fresh port
+        r = subprocess.run(cmd, cwd=str(cwd), env=env, capture_output=True, text=True, timeout=300)
+        if r.returncode != 0 and "EADDRINUSE" in r.stderr and "--master-port" in cmd:
+            cmd[cmd.index("--master-port") + 1] = str(free_port())
+            continue
+        break
     assert r.returncode == 0, r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1

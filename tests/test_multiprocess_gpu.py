@@ -27,9 +27,15 @@ def _env():
 
 
 def _torchrun(n, script_args, cwd, timeout=400):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
-           "127.0.0.1", "--master-port", str(free_port()), *script_args]
-    r = subprocess.run(cmd, cwd=cwd, env=_env(), capture_output=True, text=True, timeout=timeout)
+    # a port from free_port() can be taken again before the launcher binds it: retry on that
+    # (and only that) with a fresh port
+    for _attempt in range(3):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+               "127.0.0.1", "--master-port", str(free_port()), *script_args]
+        r = subprocess.run(cmd, cwd=cwd, env=_env(), capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0 and "EADDRINUSE" in r.stderr:
+            continue
+        break
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     return r.stdout
 
