@@ -19,7 +19,12 @@ def pytest_configure(config):
     if os.environ.get("HEAT2D_NO_BUILD") != "1":
         from heat2d_amd import _build
 
-        _build.build(cli=True)
+        # binaries stamped with the current source hash are up to date: no compile step (a GPU
+        # box receives the built extension and CLI but not build/obj, so an object-level
+        # incremental build there would recompile everything)
+        want = _build.source_hash()
+        if _build.stamped_hash(_build.EXT_PATH) != want or _build.stamped_hash(_build.CLI_PATH) != want:
+            _build.build(cli=True)
 
 
 @pytest.fixture(scope="session")
