@@ -59,9 +59,10 @@ def main() -> int:
     ap.add_argument("--layout", choices=("rows", "blocks"), default=None, help="override the config's layout")
     ap.add_argument("--precision", choices=("ref", "fp32"), default="ref")
     ap.add_argument("--boundary", choices=("fixed", "ghost-zero"), default="fixed")
-    # halo depth = deepest chunk: 7 measured best at 4096^2 (1000 steps: 7.62-7.72 vs 7.89-7.93 us/step
-    # with 8; 20 steps run as 7+7+6 either way; profiles/tblock_sweep_r2.txt)
-    ap.add_argument("--tblock", type=int, default=7)
+    # halo depth = deepest chunk, measured at 4096^2 (profiles/tblock_sweep_r2.txt): ref 7 (1000 steps
+    # 7.57-7.66 vs 7.61-7.78 us/step with 8; 20 steps run as 7+7+6 either way), fp32 8 (4.35e12 vs
+    # 3.79e12 cell-updates/s with 7)
+    ap.add_argument("--tblock", type=int, default=0, help="halo depth / deepest chunk (0: 7 for ref, 8 for fp32)")
     ap.add_argument("--rows-per-wave", type=int, default=0)
     ap.add_argument("--transport", choices=("auto", "ipc", "rccl", "torch", "host"), default="auto")
     ap.add_argument("--pipeline", choices=("auto", "signal", "concurrent", "boundary-first", "serial"), default="auto")
@@ -77,6 +78,8 @@ def main() -> int:
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: rehearsal of the distributed contract on the host (gloo), not a benchmark")
     a = ap.parse_args()
+    if a.tblock <= 0:
+        a.tblock = 8 if a.precision == "fp32" else 7
 
     import numpy as np
     import torch
