@@ -43,7 +43,7 @@ class Config:
     text_style: str = "grad"
     device: str = "auto"  # auto | gpu | cpu
     transport: str = "auto"  # auto | local | ipc | rccl | torch | host
-    tblock: int = 8
+    tblock: int = 0  # halo depth / deepest chunk; 0: measured default (7 ref, 8 fp32)
     rows_per_wave: int = 0
     overlap: bool = True
     pipeline: str = "auto"  # auto | signal | concurrent | boundary-first | serial (multi-rank halo pipeline)
@@ -127,7 +127,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="halo transport: in-process tiles, direct IPC peer stores (1-D row strips), native RCCL, "
                         "torch.distributed p2p (nccl backend on GPUs), or host (gloo p2p with host staging; also "
                         "allows several ranks per GPU)")
-    p.add_argument("--tblock", type=int, default=8, help="time steps fused per kernel (halo depth)")
+    p.add_argument("--tblock", type=int, default=0,
+                   help="time steps fused per kernel (halo depth); 0: 7 for ref, 8 for fp32 (measured at 4096^2)")
     p.add_argument("--rows-per-wave", type=int, default=0, help="rows per wave work unit (0 = auto)")
     p.add_argument("--no-overlap", action="store_true", help="do not overlap halo exchange with interior compute")
     p.add_argument("--pipeline", choices=("auto", "signal", "concurrent", "boundary-first", "serial"), default="auto",

@@ -286,7 +286,8 @@ int main(int argc, char** argv) {
   const std::string per = a.count("periodic") ? a["periodic"] : "none";
   o.periodic_x = per.find('x') != std::string::npos;
   o.periodic_y = per.find('y') != std::string::npos;
-  o.tblock = (int)geti("tblock", 8);
+  o.tblock = (int)geti("tblock", 0);
+  if (o.tblock <= 0) o.tblock = o.precision == kFp32 ? 8 : 7;  // measured at 4096^2 (profiles/tblock_sweep_r2.txt)
   o.rows_per_wave = (int)geti("rows-per-wave", 0);
   o.overlap = !a.count("no-overlap");
   int ndev = 0;

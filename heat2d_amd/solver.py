@@ -198,7 +198,7 @@ class Solver:
         cfg, n = self.cfg, native()
         from .utils.benchmark import PIPELINE_OPTIONS
 
-        kw = dict(tblock=cfg.tblock, rows_per_wave=cfg.rows_per_wave, small_grid_lds=cfg.small_grid,
+        kw = dict(tblock=cfg.tblock if cfg.tblock > 0 else (8 if cfg.precision == "fp32" else 7), rows_per_wave=cfg.rows_per_wave, small_grid_lds=cfg.small_grid,
                   tiled={"auto": -1, "on": 1, "off": 0}[cfg.tiled], overlap=cfg.overlap)
         if cfg.pipeline not in PIPELINE_OPTIONS:
             raise ValueError(f"unknown pipeline {cfg.pipeline!r}")
