@@ -72,9 +72,10 @@ def main() -> int:
     ap.add_argument("--repeat", type=int, default=3,
                     help="timed runs of exactly --steps steps each; the MEDIAN is reported (a 20-step run lasts "
                          "~170 us, so one host hiccup would otherwise decide the number), all are in repeats_s")
-    ap.add_argument("--prewarm-s", type=float, default=0.3,
+    ap.add_argument("--prewarm-s", type=float, default=1.5,
                     help="seconds of untimed stencil work before the warm-up steps, so the GPU reaches its "
-                         "steady power state (the first ~10 ms after idle run at lower clocks)")
+                         "steady power state: with 0.3 s, the first bench on a box that had been idle timed "
+                         "236/194/180 us for its three 20-step runs (steady: ~171 us)")
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: rehearsal of the distributed contract on the host (gloo), not a benchmark")
     a = ap.parse_args()
