@@ -76,6 +76,8 @@ def main() -> int:
                     help="seconds of untimed stencil work before the warm-up steps, so the GPU reaches its "
                          "steady power state: with 0.3 s, the first bench on a box that had been idle timed "
                          "236/194/180 us for its three 20-step runs (steady: ~171 us)")
+    ap.add_argument("--sync-mode", type=int, default=2, choices=(0, 1, 2, 3),
+                    help="engine end-of-run synchronisation (EngineOptions::sync_mode)")
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: rehearsal of the distributed contract on the host (gloo), not a benchmark")
     a = ap.parse_args()
@@ -122,7 +124,7 @@ def main() -> int:
         return Config(preset="heat2d", nx=nx_, ny=ny_, steps=steps_, gridx=gridx, gridy=gridy, boundary=a.boundary,
                       precision=a.precision, init="exact", output="none", device=a.device, transport=transport,
                       tblock=a.tblock, rows_per_wave=a.rows_per_wave, overlap=not a.no_overlap, pipeline=pipeline,
-                      quiet=True, report="grad", text_style="grad", sync_mode=2)
+                      quiet=True, report="grad", text_style="grad", sync_mode=a.sync_mode)
 
     # ---- correctness gate + transport/pipeline choice (N > 1) ------------------------------
     cands = B.candidates(a.transport, a.pipeline, world, on_gpu, ctx.distinct_devices, layout)
