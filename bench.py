@@ -81,6 +81,7 @@ def main() -> int:
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: rehearsal of the distributed contract on the host (gloo), not a benchmark")
     a = ap.parse_args()
+    user_tblock = a.tblock
     if a.tblock <= 0:
         a.tblock = 8 if a.precision == "fp32" else 7
 
@@ -119,6 +120,12 @@ def main() -> int:
             free, _total = n.mem_info(device)
             side = B.fill_hbm_side(int(ctx.allreduce_min(free)), G=a.tblock)
     nx, ny, gx, gy = B.grid_for(world, side, scaling, layout)
+    ref_tblock = a.tblock  # depth of the in-job single-GPU reference (a whole grid / one tile)
+    if user_tblock <= 0 and a.precision == "ref" and nx // gx <= 1024:
+        # short per-rank tiles (4096^2 over >= 4 GPUs): the K-cone of ~9-17-row units favours 6
+        # (512x4096 alone: 20 steps 2.99 vs 3.12 us/step, 840 steps 2.01 vs 2.20; 1024 rows equal;
+        # 2048 rows 7 is best: profiles/small_tile_k_r2.txt)
+        a.tblock = 6
 
     def config(nx_, ny_, steps_, transport, pipeline, gridx, gridy):
         return Config(preset="heat2d", nx=nx_, ny=ny_, steps=steps_, gridx=gridx, gridy=gridy, boundary=a.boundary,
@@ -217,7 +224,7 @@ def main() -> int:
         digests = ctx.gather_objects(B.grid_digest(s.tiles()) if scaling == "strong" else None)
         if ctx.rank == 0:
             e = n.Engine(rnx, rny, boundary=0 if a.boundary == "fixed" else 1,
-                         precision=0 if a.precision == "ref" else 1, tblock=a.tblock,
+                         precision=0 if a.precision == "ref" else 1, tblock=ref_tblock,
                          rows_per_wave=a.rows_per_wave, device=device, small_grid_lds=False)
             # the same step count as the multi-GPU run, its last pre-warm run shaped like the timed one
             if prewarm_steps >= a.steps:
