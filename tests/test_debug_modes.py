@@ -201,7 +201,7 @@ def test_host_sanitizers_engine_cpu_path(native, tmp_path):
     with cf.ThreadPoolExecutor(min(8, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(compile_one, srcs))
     exe = str(tmp_path / "engine_san")
-    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-fsanitize=address,undefined", *objs, *prebuilt, "-o", exe,
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-fno-gpu-sanitize", "-fsanitize=address,undefined", *objs, *prebuilt, "-o", exe,
                         "-L/opt/rocm/lib", "-lrccl", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
