@@ -188,7 +188,9 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
         t.buf[b] = dmalloc<float>(n);
         H2D_HIP_CHECK(hipMemsetAsync(t.buf[b], 0, n * sizeof(float), compute_));
       }
-      if (fused_) {
+      // rollback copy for fused checks; a lone tile recomputes it instead (recompute_rollback),
+      // so an HBM-filling tile with the convergence check still needs only its two buffers
+      if (fused_ && !(ranks.size() == 1 && !has_exchange_)) {
         t.keep = dmalloc<float>(n);
         H2D_HIP_CHECK(hipMemsetAsync(t.keep, 0, n * sizeof(float), compute_));
         if (o.poison) launch_poison(t.g, t.keep, o.boundary == kFixed, o.periodic_x, o.periodic_y, compute_);
@@ -596,7 +598,8 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   const bool lone = fused_ && tiles_.size() == 1 && !rccl_comm_ && !direct_;
   if (fused_) {
     a.stop = d_stop_;
-    if (residual) a.keep = tl.keep;
+    // the rollback copy: a lone tile recomputes it on convergence instead (no 4 B/cell write per check)
+    if (residual && !recompute_rollback()) a.keep = tl.keep;
   }
   if (which == 0) {
     a.units = L.d_all;
@@ -1088,7 +1091,7 @@ RunStats Engine::run_impl(int64_t steps) {
       if (fused_) {
         a.stop = d_stop_;
         if (check) {
-          a.keep = T.keep + T.g.idx(0, 0);
+          a.keep = recompute_rollback() ? nullptr : T.keep + T.g.idx(0, 0);
           a.dec = decide_args(0, true);  // the last block sums the partials and decides
           decided_in_launch_ = true;
         }
@@ -1512,7 +1515,7 @@ bool Engine::check_point(int64_t steps_before, int k) {
   // the caller whether the host already sees a converged check (then it stops enqueueing;
   // launches queued after the converged one are no-ops on the device).
   const unsigned long long seq = ++chunk_seq_;
-  checks_.push_back(CheckRec{seq, steps_before, k});
+  checks_.push_back(CheckRec{seq, steps_before, k, 1 - tiles_[0].cur});  // cur has flipped past the chunk
   if (!decided_in_launch_) device_decide(seq);
   decided_in_launch_ = false;
   if (rccl_comm_) {
@@ -1534,10 +1537,22 @@ void Engine::finalize_convergence(RunStats& st) {
     // the result is the state one step before the converged check (B-5): the level K-1 rows
     // the check launch kept
     steps_done_ = it->steps_before + it->k - 1;
-    for (Tile& t : tiles_) std::swap(t.keep, t.buf[t.cur]);
     st.converged = true;
     st.residual = h_conv_->residual;
     H2D_HIP_CHECK(hipMemsetAsync(d_stop_, 0, sizeof(unsigned long long), compute_));
+    if (recompute_rollback()) {
+      // the launches after the converged check were no-ops, so the check chunk's input buffer
+      // still holds the state at steps_before: advance it k-1 steps (plain launches, no check)
+      tiles_[0].cur = it->src;
+      for (int left = it->k - 1; left > 0;) {
+        int kk = std::min(left, G_);
+        while (kk > 1 && !stream_k_supported(kk)) --kk;
+        advance(kk, false);
+        left -= kk;
+      }
+    } else {
+      for (Tile& t : tiles_) std::swap(t.keep, t.buf[t.cur]);
+    }
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
     __atomic_store_n(&h_conv_->stop_seq, 0ull, __ATOMIC_RELEASE);
     if (direct_) ipc_primed_ = false;  // the neighbours hold halos of later launches

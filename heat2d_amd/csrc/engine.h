@@ -330,7 +330,11 @@ class Engine {
     unsigned long long seq;
     int64_t steps_before;
     int k;
+    int src;  // the check chunk's input buffer (tile 0): unchanged by the no-op launches after it
   };
+  // A lone single-process tile keeps no rollback copy in its check launches: on convergence
+  // the state one step before the check is recomputed from the check chunk's input (k-1 steps).
+  bool recompute_rollback() const { return fused_ && tiles_.size() == 1 && !has_exchange_; }
   std::vector<CheckRec> checks_;
   int checks_since_sync_ = 0;
   hipEvent_t ev_check_ = nullptr;
