@@ -18,13 +18,23 @@ arithmetic exactly as the reference's C evaluates it) unless ``
 Other BASELINE rows: ``--config 8192x2rows``, ``16384x8blocks``, ``weak-4096``, ``weak-hbm``
 (per-GPU tile sized from hipMemGetInfo to fill HBM).
 
-Multi-GPU safety (N > 1): before anything is timed, every candidate (transport, pipeline) —
-the requested one, then safer fallbacks — runs a small grid of the same decomposition and
-must match the CPU oracle bit for bit on rank 0 (``heat2d_amd/utils/benchmark.py``).  The JSON
-says which one passed and what failed.  Speedup/efficiency are measured IN THIS JOB: rank 0
-re-runs the same grid (strong) or one tile (weak) on its GPU alone with the same K and W; for
-strong scaling it also replays the whole step count and compares every rank's tile with the
-single-GPU grid bit for bit (``verified``).
+Verification of what is timed: before anything else runs on the timed solver, it advances
+exactly K steps from the initial field and rank 0 compares every rank's tile with the CPU
+oracle bit for bit (grids up to ~2^30 cell-updates; larger ones verify as many leading steps as
+fit and say so).  A configuration that fails this is not timed: the next candidate is tried.
+
+Multi-GPU safety (N > 1): every candidate (transport, pipeline) — direct IPC with the measured
+fences, direct IPC with system-scope fences, RCCL, host staging — first runs a small grid of the
+same decomposition, plain and with convergence checks, and must match the CPU oracle bit for bit
+(``heat2d_amd/utils/benchmark.py``).  The JSON says which one passed and what failed.
+Speedup/efficiency are measured IN THIS JOB: rank 0 runs the same grid (strong) or one tile
+(weak) on its GPU alone with the same K and W; for strong scaling it also replays the whole step
+count and compares every rank's tile with the single-GPU grid bit for bit.  For the HBM-filling
+weak config the single-GPU tile is timed BEFORE the N-rank solver allocates (both would not fit).
+
+``halo_wait`` (N > 1, direct pipeline): the exposed halo wait of the halo units inside the
+stencil kernel (s_memrealtime around the flag poll) during the timed runs — the analogue of the
+reference's mpiP ``MPI_Waitall`` share (Report.pdf p.34-37).
 
 ``vs_baseline`` divides by the reference's best published throughput, 1.01e10 cell-updates/s
 (2560×2048, 160 MPI tasks on 20 nodes, Report.pdf p.21 Table 1 — BASELINE.md).
@@ -44,6 +54,8 @@ sys.path.insert(0, ROOT)
 # heat2d_amd/_native.py).  Read once at HIP initialisation, so it is set before torch starts.
 if os.environ.get("HEAT2D_KEEP_HW_QUEUES") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+VERIFY_BUDGET = 1 << 30  # cell-updates the CPU oracle may spend on verifying the timed solver
 
 
 def main() -> int:
@@ -65,10 +77,11 @@ def main() -> int:
     ap.add_argument("--tblock", type=int, default=0, help="halo depth / deepest chunk (0: 7 for ref, 8 for fp32)")
     ap.add_argument("--rows-per-wave", type=int, default=0)
     ap.add_argument("--transport", choices=("auto", "ipc", "rccl", "torch", "host"), default="auto")
-    ap.add_argument("--pipeline", choices=("auto", "signal", "concurrent", "boundary-first", "serial"), default="auto")
+    ap.add_argument("--pipeline", choices=("auto", "direct-sys", "signal", "serial"), default="auto")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-gate", action="store_true", help="skip the pre-timing correctness gate (N > 1)")
     ap.add_argument("--no-reference", action="store_true", help="skip the in-job single-GPU reference run")
+    ap.add_argument("--no-verify", action="store_true", help="skip the oracle check of the timed solver's first steps")
     ap.add_argument("--repeat", type=int, default=3,
                     help="timed runs of exactly --steps steps each; the MEDIAN is reported (a 20-step run lasts "
                          "~170 us, so one host hiccup would otherwise decide the number), all are in repeats_s")
@@ -85,7 +98,6 @@ def main() -> int:
     if a.tblock <= 0:
         a.tblock = 8 if a.precision == "fp32" else 7
 
-    import numpy as np
     import torch
 
     from heat2d_amd._native import native
@@ -107,6 +119,8 @@ def main() -> int:
     ctx.distinct_devices = on_gpu and world <= ndev
     if on_gpu:
         torch.cuda.set_device(device)
+    bnd = 0 if a.boundary == "fixed" else 1
+    prec = 0 if a.precision == "ref" else 1
 
     bc = B.CONFIGS[a.config]
     scaling = a.scaling or bc.scaling
@@ -127,39 +141,14 @@ def main() -> int:
         # 2048 rows 7 is best: profiles/small_tile_k_r2.txt)
         a.tblock = 6
 
-    def config(nx_, ny_, steps_, transport, pipeline, gridx, gridy):
-        return Config(preset="heat2d", nx=nx_, ny=ny_, steps=steps_, gridx=gridx, gridy=gridy, boundary=a.boundary,
-                      precision=a.precision, init="exact", output="none", device=a.device, transport=transport,
-                      tblock=a.tblock, rows_per_wave=a.rows_per_wave, overlap=not a.no_overlap, pipeline=pipeline,
-                      quiet=True, report="grad", text_style="grad", sync_mode=a.sync_mode)
-
-    # ---- correctness gate + transport/pipeline choice (N > 1) ------------------------------
-    cands = B.candidates(a.transport, a.pipeline, world, on_gpu, ctx.distinct_devices, layout)
-    gate = None
-    if world > 1 and not a.no_gate:
-        bnd = 0 if a.boundary == "fixed" else 1
-        prec = 0 if a.precision == "ref" else 1
-
-        def make_gate_solver(transport, pipeline, gnx, gny, gsteps):
-            c = config(gnx, gny, gsteps, transport, pipeline, gx, gy)
-            c.halo_timeout_s = 5.0
-            return Solver(c, ctx)
-
-        gate = B.run_gate(ctx, make_gate_solver,
-                          lambda gnx, gny, gsteps: n.oracle_run(gnx, gny, gsteps, boundary=bnd, precision=prec)["grid"],
-                          cands, gx, gy, a.tblock, log=lambda m: print(m, file=sys.stderr, flush=True))
-        if not gate.ok:
-            if ctx.rank == 0:
-                print(json.dumps({"error": "no transport passed the correctness gate", "gate": gate.tried}), flush=True)
-            ctx.shutdown()
-            return 3
-        transport, pipeline = gate.transport, gate.pipeline
-    else:
-        transport, pipeline = cands[0]
-    transport_cfg = "auto" if transport == "local" else transport
-
-    cfg = config(nx, ny, a.steps, transport_cfg, pipeline, gx, gy)
-    s = Solver(cfg, ctx)
+    def config(nx_, ny_, steps_, transport, pipeline, gridx, gridy, conv=False):
+        c = Config(preset="heat2d", nx=nx_, ny=ny_, steps=steps_, gridx=gridx, gridy=gridy, boundary=a.boundary,
+                   precision=a.precision, init="exact", output="none", device=a.device, transport=transport,
+                   tblock=a.tblock, rows_per_wave=a.rows_per_wave, overlap=not a.no_overlap, pipeline=pipeline,
+                   quiet=True, report="grad", text_style="grad", sync_mode=a.sync_mode)
+        if conv:  # checks every G+1 steps that never converge (gate only)
+            c.convergence, c.interval, c.sensitivity = True, a.tblock + 1, 0.0
+        return c
 
     def sync():
         if on_gpu:
@@ -174,13 +163,107 @@ def main() -> int:
         # host-level alignment: node-local spin barrier (exit skew ~1 us instead of gloo's tens)
         ctx.node_barrier()
 
-    # ---- pre-warm (untimed, time-based, collectively agreed count) + W warm-up steps --------
-    # The pre-warm replays the timed run's exact shape (runs of K steps: the same chunk depths,
-    # so the same kernel code is hot in the caches) until the GPU has been busy ~prewarm_s.
+    def solo_timed(e):
+        """One engine alone (rank 0's in-job reference): the time-based pre-warm, the W warm-up
+        steps, then the median of `repeat` timed runs of exactly --steps steps."""
+        if on_gpu and a.prewarm_s > 0 and a.steps > 0:
+            t0 = time.perf_counter()
+            e.run(a.steps)
+            e.synchronize()
+            for _ in range(max(0, min(20000, math.ceil(a.prewarm_s / max(time.perf_counter() - t0, 1e-6)) - 1))):
+                e.run(a.steps)
+        if a.warmup > 0:
+            e.run(a.warmup)
+        ts = []
+        for _ in range(max(1, a.repeat)):
+            e.synchronize()
+            t0 = time.perf_counter()
+            e.run(a.steps)
+            e.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[(len(ts) - 1) // 2]
+
+    # ---- weak-hbm: the single-GPU reference tile BEFORE the N-rank solver allocates ----------
+    t1_pre = None
+    if world > 1 and fill_hbm and not a.no_reference:
+        if ctx.rank == 0:
+            e = n.Engine(side, side, boundary=bnd, precision=prec, tblock=ref_tblock, rows_per_wave=a.rows_per_wave,
+                         device=device, small_grid_lds=False, sync_mode=a.sync_mode)
+            t1_pre = solo_timed(e)
+            del e
+        ctx.barrier()
+
+    # ---- candidate choice: correctness gate, then the timed solver itself must verify --------
+    verify_steps = 0
+    cells = nx * ny
+    if not a.no_verify and a.steps > 0 and cells <= VERIFY_BUDGET:
+        verify_steps = max(1, min(a.steps, VERIFY_BUDGET // cells))
+    holder = {}
+
+    def build_timed(transport, pipeline):
+        """Collective: the timed solver, and its first `verify_steps` steps from the initial field
+        checked against the CPU oracle on rank 0.  (ok on this rank, why not)."""
+        if "solver" in holder:
+            holder.pop("solver").close()
+        try:
+            s = Solver(config(nx, ny, a.steps, "auto" if transport == "local" else transport, pipeline, gx, gy), ctx)
+        except Exception as ex:  # noqa: BLE001 - e.g. a timed strip too short for the transport
+            ctx.allreduce_min(0)  # pair with the agreement below on the other ranks
+            return 0, f"timed solver: {type(ex).__name__}: {ex}"
+        if ctx.allreduce_min(1) < 1:
+            s.close()
+            return 0, "timed solver failed on another rank"
+        holder["solver"] = s
+        holder["verified"] = None
+        if verify_steps > 0:
+            s.run_steps(verify_steps)
+            digests = ctx.gather_objects(B.grid_digest(s.tiles()))
+            ok = 1
+            if ctx.rank == 0:
+                ref = n.oracle_run(nx, ny, verify_steps, boundary=bnd, precision=prec)["grid"]
+                ok = int(all(B.digest_of_region(ref, k) == v for d in digests for k, v in d.items()))
+            ok = int(ctx.allreduce_min(ok))
+            holder["verified"] = bool(ok)
+            if not ok:
+                return 0, f"the timed solver's first {verify_steps} steps differ from the CPU oracle"
+        return 1, ""
+
+    rows_per_rank = nx // gx
+    cands = B.candidates(a.transport, a.pipeline, world, on_gpu, ctx.distinct_devices, layout,
+                         rows_per_rank=rows_per_rank, depth=a.tblock)
+    gate = None
+    log = lambda m: print(m, file=sys.stderr, flush=True)  # noqa: E731
+    if world > 1 and not a.no_gate:
+        def make_gate_solver(transport, pipeline, gnx, gny, gsteps, conv=False):
+            c = config(gnx, gny, gsteps, transport, pipeline, gx, gy, conv=conv)
+            c.halo_timeout_s = 5.0
+            return Solver(c, ctx)
+
+        gate = B.run_gate(ctx, make_gate_solver,
+                          lambda gnx, gny, gsteps: n.oracle_run(gnx, gny, gsteps, boundary=bnd, precision=prec)["grid"],
+                          cands, gx, gy, a.tblock, log=log, accept=build_timed)
+        if not gate.ok:
+            if ctx.rank == 0:
+                print(json.dumps({"error": "no transport passed the correctness gate", "gate": gate.tried}), flush=True)
+            ctx.shutdown()
+            return 3
+        transport, pipeline = gate.transport, gate.pipeline
+    else:
+        transport, pipeline = cands[0]
+        ok, why = build_timed(transport, pipeline)
+        if not ok:
+            if ctx.rank == 0:
+                print(json.dumps({"error": why, "transport": transport, "pipeline": pipeline}), flush=True)
+            ctx.shutdown()
+            return 3
+    s = holder["solver"]
+    verified_first = holder["verified"]
+
+    # ---- pre-warm + warm-up + timed region ----------------------------------------------------
     run = s.run_steps
+    times = []
     prewarm_steps = 0
     if on_gpu and a.prewarm_s > 0 and a.steps > 0:
-        # ranks that ran different step counts would post unmatched halo sends and deadlock
         sync_barrier()
         t0 = time.perf_counter()
         run(a.steps)
@@ -193,40 +276,57 @@ def main() -> int:
         sync_barrier()
     if a.warmup > 0:
         run(a.warmup)
-
-    # ---- timed region -----------------------------------------------------------------------
-    res, times = None, []
+    if on_gpu:
+        s.engine.reset_halo_wait()  # the halo-wait counters describe the timed runs only
+    res = None
     for _ in range(max(1, a.repeat)):
         sync_barrier()
         t0 = time.perf_counter()
         res = run(a.steps)
         sync()
-        dt = ctx.allreduce_max(time.perf_counter() - t0)
-        times.append(dt)
+        times.append(ctx.allreduce_max(time.perf_counter() - t0))
     best = sorted(times)[(len(times) - 1) // 2]  # median (lower median for an even count)
-    total_steps = prewarm_steps + max(0, a.warmup) + a.steps * max(1, a.repeat)
+    total_steps = verify_steps + prewarm_steps + max(0, a.warmup) + a.steps * max(1, a.repeat)
     if res["steps_done"] != total_steps:
         raise SystemExit(f"bench: step accounting error ({res['steps_done']} != {total_steps})")
     cups = float(nx) * float(ny) * a.steps / best
     pipeline_used = s.engine.pipeline()
     halo_depth = s.engine.halo_depth()
     path = res["path"]
+    halo_wait = None
+    if on_gpu and world > 1:
+        hw = s.engine.halo_wait()
+        chunks = max(1, int(res["chunks"]))
+        chunk_us = best * 1e6 / chunks
+        mine = (hw["total_us"] / max(1, hw["waits"]), hw["max_us"], hw["waits"])
+        allw = ctx.gather_objects(mine)
+        if ctx.rank == 0 and hw is not None:
+            mean_max = max(w[0] for w in allw)
+            halo_wait = {"mean_us_per_halo_unit": mean_max, "max_us": max(w[1] for w in allw),
+                         "waits_per_rank": [int(w[2]) for w in allw], "chunk_us": chunk_us,
+                         "share_of_chunk": mean_max / chunk_us if chunk_us > 0 else None,
+                         "note": "worst rank; in-kernel flag-poll time of the halo units during the timed runs "
+                                 "(Report.pdf p.34-37 MPI_Waitall analogue)"}
 
     # ---- in-job single-GPU reference: speedup / efficiency, and bit-exact verification ------
     t1 = None
-    verified = None
+    verified_full = None
     ref_note = None
     if world == 1:
         t1 = best
+    elif fill_hbm and not a.no_reference:
+        t1 = t1_pre  # rank 0 only
+        ref_note = "rank 0's GPU alone, one tile, same K/W, measured in this job before the N-rank solver"
     elif not a.no_reference and not fill_hbm:
         # strong: the same global grid on rank 0's GPU alone; weak: one GPU's tile alone
         rnx, rny = (nx, ny) if scaling == "strong" else (side, side)
         digests = ctx.gather_objects(B.grid_digest(s.tiles()) if scaling == "strong" else None)
         if ctx.rank == 0:
-            e = n.Engine(rnx, rny, boundary=0 if a.boundary == "fixed" else 1,
-                         precision=0 if a.precision == "ref" else 1, tblock=ref_tblock,
-                         rows_per_wave=a.rows_per_wave, device=device, small_grid_lds=False)
+            e = n.Engine(rnx, rny, boundary=bnd, precision=prec, tblock=ref_tblock, rows_per_wave=a.rows_per_wave,
+                         device=device, small_grid_lds=False)
             # the same step count as the multi-GPU run, its last pre-warm run shaped like the timed one
+            if verify_steps > 0:
+                e.run(verify_steps)
             if prewarm_steps >= a.steps:
                 e.run(prewarm_steps - a.steps) if prewarm_steps > a.steps else None
                 e.run(a.steps)
@@ -244,7 +344,7 @@ def main() -> int:
             t1 = sorted(ts)[(len(ts) - 1) // 2]
             if scaling == "strong":
                 full = e.download(0)
-                verified = all(B.digest_of_region(full, k) == v for d in digests for k, v in d.items())
+                verified_full = all(B.digest_of_region(full, k) == v for d in digests for k, v in d.items())
             ref_note = (f"rank 0's GPU alone, {'same grid' if scaling == 'strong' else 'one tile'}, "
                         f"same K/W, measured in this job")
             del e
@@ -261,6 +361,14 @@ def main() -> int:
                 speedup = eff * world
         else:
             speedup = eff = None
+        checks = [v for v in (verified_first, verified_full) if v is not None]
+        verified = all(checks) if checks else None
+        how = []
+        if verified_first is not None:
+            how.append(f"first {verify_steps} steps of the timed solver == CPU oracle "
+                       f"({'all' if verify_steps == a.steps else 'leading'} {verify_steps} of --steps {a.steps})")
+        if verified_full is not None:
+            how.append(f"after all {total_steps} steps every rank's tile == rank 0's single-GPU run")
         out = {
             "metric": B.metric_label(nx, ny, a.steps),
             "value": cups,
@@ -277,6 +385,7 @@ def main() -> int:
             "t1_ms_per_step": (t1 * 1e3 / a.steps) if t1 is not None else None,
             "speedup_reference": ref_note or ("this run (N=1)" if world == 1 else None),
             "verified": verified,
+            "verification": "; ".join(how) if how else "none (grid too large for the oracle and no in-job reference)",
             "dtype": "fp32",
             "compute": ("fp64 expression, bit-exact with the reference" if a.precision == "ref" else "fp32 FMA"),
             "data": "synthetic center-hot initial field (exact formula, generated on device)",
@@ -285,6 +394,7 @@ def main() -> int:
             "timing": f"median of {len(times)} timed runs of exactly {a.steps} steps (max over ranks each)",
             "prewarm_steps": prewarm_steps,
             "gate": (gate.tried if gate is not None else None),
+            "halo_wait": halo_wait,
             "config": {
                 "name": a.config,
                 "model": ("heat2d 5-point Jacobi, fixed edges" if a.boundary == "fixed"
@@ -296,6 +406,7 @@ def main() -> int:
                 "parallelism": B.parallelism_label(world, gx, gy),
                 "transport": transport,
                 "pipeline": pipeline_used,
+                "candidate": f"{transport}/{pipeline}",
                 "tblock": halo_depth,
                 "path": path,
                 "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),

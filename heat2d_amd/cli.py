@@ -14,7 +14,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     # stream.  The engine runs compute and comm streams concurrently and HIP maps streams onto
     # at most GPU_MAX_HW_QUEUES in-order hardware queues; with 4, other libraries' streams can
     # shift the round-robin map until compute and comm share one queue, which serialises the
-    # exchange behind the stencil (measured 9.5 -> 15 us/step, tools/gpu_probe_queues.sh).
+    # exchange behind the stencil (measured 9.5 -> 15 us/step in round 1).
     # Read once at HIP initialisation, i.e. before the first HIP call of the process.
     import os
 

@@ -46,7 +46,7 @@ class Config:
     tblock: int = 0  # halo depth / deepest chunk; 0: measured default (7 ref, 8 fp32)
     rows_per_wave: int = 0
     overlap: bool = True
-    pipeline: str = "auto"  # auto | signal | concurrent | boundary-first | serial (multi-rank halo pipeline)
+    pipeline: str = "auto"  # auto | direct-sys | signal | serial (multi-rank halo pipeline)
     sync_mode: int = 0  # end-of-run synchronisation (EngineOptions::sync_mode; the bench uses 2)
     halo_timeout_s: float = 30.0  # bounded device-side halo waits give up (and the run fails) after this
     small_grid: bool = True
@@ -131,8 +131,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="time steps fused per kernel (halo depth); 0: 7 for ref, 8 for fp32 (measured at 4096^2)")
     p.add_argument("--rows-per-wave", type=int, default=0, help="rows per wave work unit (0 = auto)")
     p.add_argument("--no-overlap", action="store_true", help="do not overlap halo exchange with interior compute")
-    p.add_argument("--pipeline", choices=("auto", "signal", "concurrent", "boundary-first", "serial"), default="auto",
-                   help="multi-rank halo pipeline (auto: the transport's default)")
+    p.add_argument("--pipeline", choices=("auto", "direct-sys", "signal", "serial"), default="auto",
+                   help="multi-rank halo pipeline (auto: the transport's default; direct-sys: the direct IPC "
+                        "pipeline with system-scope fences; signal / serial: RCCL pipelines)")
     p.add_argument("--no-small-grid", action="store_true", help="disable the whole-grid LDS solver")
     p.add_argument("--tiled", choices=("auto", "on", "off"), default="auto",
                    help="LDS-tiled temporally-blocked kernel for single-tile small/medium grids")

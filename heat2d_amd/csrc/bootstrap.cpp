@@ -5,9 +5,14 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <cerrno>
+#include <cstdlib>
+
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -31,10 +36,26 @@ void recv_all(int fd, void* p, size_t n) {
   char* c = static_cast<char*>(p);
   while (n > 0) {
     const ssize_t k = ::recv(fd, c, n, 0);
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK))
+      throw std::runtime_error("bootstrap: receive timed out (a peer stopped taking part)");
     if (k <= 0) throw std::runtime_error("bootstrap: receive failed (peer gone?)");
     c += k;
     n -= (size_t)k;
   }
+}
+
+// Bound every later receive on fd (SO_RCVTIMEO): a hung peer fails the collective instead of
+// blocking this rank forever.
+void recv_timeout(int fd, double s) {
+  timeval tv{};
+  tv.tv_sec = (time_t)s;
+  tv.tv_usec = (suseconds_t)((s - (double)tv.tv_sec) * 1e6);
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+}
+
+template <class TP>
+double remaining(TP deadline) {
+  return std::chrono::duration<double>(deadline - std::chrono::steady_clock::now()).count();
 }
 
 void send_blob(int fd, const std::string& s) {
@@ -98,7 +119,8 @@ RankEnv rank_env() {
   return e;
 }
 
-Bootstrap::Bootstrap(int rank, int world, const std::string& addr, int port, double timeout_s)
+Bootstrap::Bootstrap(int rank, int world, const std::string& addr, int port, double timeout_s,
+                     double io_timeout_s)
     : rank_(rank), world_(world) {
   if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("bootstrap: bad rank / world size");
   if (world == 1) return;
@@ -114,24 +136,37 @@ Bootstrap::Bootstrap(int rank, int world, const std::string& addr, int port, dou
     freeaddrinfo(res);
   }
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  if (const char* v = std::getenv("HEAT2D_BOOT_IO_TIMEOUT_S")) io_timeout_s = std::atof(v);
   if (rank == 0) {
-    listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
-    int one = 1;
-    setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-    if (::bind(listen_fd_, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0)
-      throw std::runtime_error("bootstrap: rank 0 cannot bind port " + std::to_string(port));
-    ::listen(listen_fd_, world);
+    const char* inherited = std::getenv("HEAT2D_BOOT_LISTEN_FD");
+    if (inherited != nullptr) {
+      listen_fd_ = std::atoi(inherited);  // bound and listening (heat2d --np)
+    } else {
+      // no SO_REUSEADDR: a second job on the same port fails here instead of pairing ranks
+      listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+      if (::bind(listen_fd_, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0)
+        throw std::runtime_error("bootstrap: rank 0 cannot bind port " + std::to_string(port) + " (in use?)");
+      ::listen(listen_fd_, world);
+    }
     fds_.assign(world, -1);
     for (int i = 1; i < world; ++i) {
+      pollfd pf{listen_fd_, POLLIN, 0};
+      const double left = remaining(deadline);
+      if (left <= 0 || ::poll(&pf, 1, (int)(left * 1000.0) + 1) <= 0)
+        throw std::runtime_error("bootstrap: rank 0 timed out waiting for " + std::to_string(world - i) +
+                                 " rank(s) to connect");
       const int fd = ::accept(listen_fd_, nullptr, nullptr);
       if (fd < 0) throw std::runtime_error("bootstrap: accept failed");
       nodelay(fd);
+      recv_timeout(fd, std::max(1.0, remaining(deadline)));
       int32_t r = -1;
       recv_all(fd, &r, sizeof(r));
       if (r <= 0 || r >= world || fds_[r] >= 0) throw std::runtime_error("bootstrap: bad peer rank");
       fds_[r] = fd;
     }
+    for (int r = 1; r < world; ++r) recv_timeout(fds_[r], io_timeout_s);
   } else {
+    if (const char* inherited = std::getenv("HEAT2D_BOOT_LISTEN_FD")) ::close(std::atoi(inherited));
     int fd = -1;
     for (;;) {
       fd = ::socket(AF_INET, SOCK_STREAM, 0);
@@ -143,6 +178,7 @@ Bootstrap::Bootstrap(int rank, int world, const std::string& addr, int port, dou
       std::this_thread::sleep_for(std::chrono::milliseconds(20));
     }
     nodelay(fd);
+    recv_timeout(fd, io_timeout_s);
     const int32_t r = rank;
     send_all(fd, &r, sizeof(r));
     fds_.assign(1, fd);

@@ -22,8 +22,12 @@ namespace h2d {
 
 class Bootstrap {
  public:
-  // rank 0 listens on addr:port; the others connect (retrying until timeout_s)
-  Bootstrap(int rank, int world, const std::string& addr, int port, double timeout_s = 120.0);
+  // rank 0 listens on addr:port (or on the socket HEAT2D_BOOT_LISTEN_FD names, which `heat2d --np`
+  // binds before forking: no port race); the others connect.  Every wait is bounded: connecting
+  // and accepting by timeout_s, every later receive by io_timeout_s (a collective can legitimately
+  // wait as long as a run lasts; env HEAT2D_BOOT_IO_TIMEOUT_S overrides it).
+  Bootstrap(int rank, int world, const std::string& addr, int port, double timeout_s = 120.0,
+            double io_timeout_s = 3600.0);
   ~Bootstrap();
   Bootstrap(const Bootstrap&) = delete;
   Bootstrap& operator=(const Bootstrap&) = delete;

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <limits>
 #include <stdexcept>
+#include <thread>
 
 namespace h2d {
 
@@ -49,18 +50,32 @@ OracleResult oracle_run(int64_t NX, int64_t NY, int64_t steps, const Physics& ph
   std::vector<float>* cur = &a;
   std::vector<float>* nxt = &b;
   int64_t done = 0;
+  // Large grids (the bench's verification of a 4096^2 run) update row blocks on several
+  // threads: every cell is independent within a step, so the result is the same bits.
+  const int nthreads = NX * NY >= (int64_t)1 << 20
+                           ? (int)std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency()))
+                           : 1;
   for (int64_t k = 0; k < steps; ++k) {
     fill_ring(*cur);
     const std::vector<float>& u = *cur;
     std::vector<float>& v = *nxt;
-    for (int64_t i = 0; i < NX; ++i) {
-      const int rm = dim_mode(i, NX, ph.periodic_x, fixed);
-      for (int64_t j = 0; j < NY; ++j) {
-        const int m = std::max(rm, dim_mode(j, NY, ph.periodic_y, fixed));
-        const size_t c = (size_t)((i + 1) * P + (j + 1));
-        if (m == 0) v[c] = cell_update(ph, u[c], u[c - P], u[c + P], u[c - 1], u[c + 1]);
-        else v[c] = u[c];
+    auto rows = [&](int64_t i0, int64_t i1) {
+      for (int64_t i = i0; i < i1; ++i) {
+        const int rm = dim_mode(i, NX, ph.periodic_x, fixed);
+        for (int64_t j = 0; j < NY; ++j) {
+          const int m = std::max(rm, dim_mode(j, NY, ph.periodic_y, fixed));
+          const size_t c = (size_t)((i + 1) * P + (j + 1));
+          if (m == 0) v[c] = cell_update(ph, u[c], u[c - P], u[c + P], u[c - 1], u[c + 1]);
+          else v[c] = u[c];
+        }
       }
+    };
+    if (nthreads > 1) {
+      std::vector<std::thread> pool;
+      for (int t = 0; t < nthreads; ++t) pool.emplace_back(rows, NX * t / nthreads, NX * (t + 1) / nthreads);
+      for (auto& th : pool) th.join();
+    } else {
+      rows(0, NX);
     }
     const int64_t committed = k + 1;
     if (convergence && interval > 0 && committed % interval == 0) {

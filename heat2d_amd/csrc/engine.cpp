@@ -165,6 +165,12 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     H2D_HIP_CHECK(hipHostMalloc(&h_resid_, sizeof(double) * (ranks.size() + 1)));
     d_lds_steps_ = dmalloc<long long>(1);
     d_dummy_ = dmalloc<float>(4 * kWaveCols);
+    d_wait_acc_ = dmalloc<unsigned long long>(4);
+    H2D_HIP_CHECK(hipMemset(d_wait_acc_, 0, 4 * sizeof(unsigned long long)));
+    if (o.timeline > 0) {
+      if (o.timeline > 4096) throw std::invalid_argument("timeline: at most 4096 launches");
+      d_stamps_ = dmalloc<unsigned long long>((size_t)o.timeline * kTimelineUnits * 4);
+    }
     if (o.convergence && !o.naive && transport_ != kTransportExternal && o.fused_check != 0) {
       d_stop_ = dmalloc<unsigned long long>(1);
       H2D_HIP_CHECK(hipMemset(d_stop_, 0, sizeof(unsigned long long)));
@@ -392,6 +398,8 @@ Engine::~Engine() {
   hipHostFree(h_resid_);
   hipFree(d_lds_steps_);
   hipFree(d_dummy_);
+  hipFree(d_wait_acc_);
+  if (d_stamps_) hipFree(d_stamps_);
   hipFree(d_send_);
   hipFree(d_recv_);
   hipEventDestroy(ev_ready_);
@@ -658,6 +666,11 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
         a.need[0] = a.need[1] = halo_seq_;
       }
     }
+  }
+  a.wait_acc = d_wait_acc_;
+  if (d_stamps_ != nullptr && (int)tl_recs_.size() < opt_.timeline && a.nunits <= kTimelineUnits) {
+    a.stamps = d_stamps_ + tl_recs_.size() * (size_t)kTimelineUnits * 4;
+    tl_recs_.emplace_back(K, a.nunits);
   }
   launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
   progress_tick(stream ? stream : compute_);
@@ -1032,6 +1045,7 @@ RunStats Engine::run_impl(int64_t steps) {
   RunStats st;
   const auto w0 = std::chrono::steady_clock::now();
   const int64_t target = steps_done_ + steps;
+  tl_recs_.clear();
 
   if (!on_gpu()) {
     st.path = "cpu";
@@ -1465,7 +1479,7 @@ RunStats Engine::run_impl(int64_t steps) {
   }
   end_of_run_wait(st, w0);
   poll_abort();
-  if (fused_) finalize_convergence(st);
+  if (fused_ && finalize_convergence(st)) end_of_run_wait(st, w0);  // times include the recompute launches
   trace_collect(st);
   st.steps_done = steps_done_;
   return st;
@@ -1529,7 +1543,8 @@ bool Engine::check_point(int64_t steps_before, int k) {
   return __atomic_load_n(&h_conv_->stop_seq, __ATOMIC_ACQUIRE) != 0ull;
 }
 
-void Engine::finalize_convergence(RunStats& st) {
+bool Engine::finalize_convergence(RunStats& st) {
+  bool launched = false;
   const unsigned long long seq = __atomic_load_n(&h_conv_->stop_seq, __ATOMIC_ACQUIRE);
   if (seq != 0ull) {
     auto it = std::find_if(checks_.begin(), checks_.end(), [&](const CheckRec& r) { return r.seq == seq; });
@@ -1544,6 +1559,7 @@ void Engine::finalize_convergence(RunStats& st) {
       // the launches after the converged check were no-ops, so the check chunk's input buffer
       // still holds the state at steps_before: advance it k-1 steps (plain launches, no check)
       tiles_[0].cur = it->src;
+      launched = it->k > 1;
       for (int left = it->k - 1; left > 0;) {
         int kk = std::min(left, G_);
         while (kk > 1 && !stream_k_supported(kk)) --kk;
@@ -1561,6 +1577,7 @@ void Engine::finalize_convergence(RunStats& st) {
   }
   checks_.clear();
   checks_since_sync_ = 0;
+  return launched;
 }
 
 void Engine::end_of_run_wait(RunStats& st, std::chrono::steady_clock::time_point w0) {
@@ -1688,6 +1705,51 @@ void Engine::synchronize() const {
     H2D_HIP_CHECK(hipStreamSynchronize(comm_));
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
   }
+}
+
+Engine::HaloWait Engine::halo_wait() const {
+  HaloWait h;
+  if (!on_gpu()) return h;
+  synchronize();
+  unsigned long long v[3] = {0, 0, 0};
+  H2D_HIP_CHECK(hipMemcpy(v, d_wait_acc_, sizeof(v), hipMemcpyDeviceToHost));
+  h.total_us = (double)v[0] * 0.01;  // s_memrealtime: 100 MHz
+  h.waits = (int64_t)v[1];
+  h.max_us = (double)v[2] * 0.01;
+  return h;
+}
+
+void Engine::reset_halo_wait() {
+  if (!on_gpu()) return;
+  synchronize();
+  H2D_HIP_CHECK(hipMemset(d_wait_acc_, 0, 4 * sizeof(unsigned long long)));
+}
+
+std::vector<Unit> Engine::unit_list(int t, int K, int which) {
+  check_tile(t);
+  if (!on_gpu()) throw std::runtime_error("unit_list: GPU engines only");
+  if (!stream_k_supported(K) || K > G_) throw std::invalid_argument("unit_list: unsupported depth");
+  const UnitLists& L = units(t, K);
+  std::vector<Unit> v((size_t)L.n_all);
+  if (!v.empty())
+    H2D_HIP_CHECK(hipMemcpy(v.data(), which == 3 ? L.d_bfirst : L.d_all, v.size() * sizeof(Unit), hipMemcpyDeviceToHost));
+  return v;
+}
+
+std::vector<Engine::LaunchTimeline> Engine::timeline() const {
+  std::vector<LaunchTimeline> out;
+  if (!on_gpu() || d_stamps_ == nullptr) return out;
+  synchronize();
+  for (size_t i = 0; i < tl_recs_.size(); ++i) {
+    LaunchTimeline t;
+    t.K = tl_recs_[i].first;
+    t.units = tl_recs_[i].second;
+    t.stamps.resize((size_t)t.units * 4);
+    H2D_HIP_CHECK(hipMemcpy(t.stamps.data(), d_stamps_ + i * (size_t)kTimelineUnits * 4,
+                            t.stamps.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    out.push_back(std::move(t));
+  }
+  return out;
 }
 
 std::string Engine::rccl_unique_id() {

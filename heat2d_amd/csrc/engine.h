@@ -95,6 +95,9 @@ struct EngineOptions {
   int wt_store = -1;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
+  // Diagnostics: record the per-wave timeline (s_memrealtime stamps) of the first `timeline`
+  // streaming launches of each run (0: off).  Read back with Engine::timeline().
+  int timeline = 0;
   bool poison = false;        // debug canary: NaN in every cell no valid update may read
   bool convergence = false;
   int64_t interval = 20;
@@ -207,6 +210,24 @@ class Engine {
   void upload(int t, const float* owned);
   void synchronize() const;
 
+  // Exposed halo wait of the halo units (direct / signalled pipelines) since the last reset:
+  // {total wait in us, waits, longest wait in us}.  Synchronises; not for the timed region.
+  struct HaloWait {
+    double total_us = 0.0, max_us = 0.0;
+    int64_t waits = 0;
+  };
+  HaloWait halo_wait() const;
+  void reset_halo_wait();
+  // Per-wave timeline of the launches recorded by the last run (EngineOptions::timeline):
+  // {K, units, stamps[units][4] = start, ready (halo wait done), end, hardware id}.
+  struct LaunchTimeline {
+    int K = 0, units = 0;
+    std::vector<unsigned long long> stamps;
+  };
+  std::vector<LaunchTimeline> timeline() const;
+  // The work units of tile t at depth K in launch order (which: 0 all, 3 halo units first).
+  std::vector<Unit> unit_list(int t, int K, int which);
+
  private:
   struct Tile {
     int rank = 0;
@@ -278,6 +299,10 @@ class Engine {
   std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> local_descs_;  // (K, parity)
   std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> pack_descs_;   // (K, parity) for rccl
   std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> unpack_descs_;
+  unsigned long long* d_wait_acc_ = nullptr;  // StreamArgs::wait_acc (3 words)
+  unsigned long long* d_stamps_ = nullptr;    // StreamArgs::stamps ring (timeline diagnostics)
+  static constexpr int kTimelineUnits = 8192; // units recorded per launch at most
+  std::vector<std::pair<int, int>> tl_recs_;  // (K, units) of each launch recorded this run
   double* d_resid_ = nullptr;       // [num_tiles] + 1 total
   double* h_resid_ = nullptr;       // pinned
   long long* d_lds_steps_ = nullptr;
@@ -345,7 +370,7 @@ class Engine {
   DecideArgs decide_args(int t, bool decide) const;
   void device_decide(unsigned long long seq);
   bool check_point(int64_t steps_before, int k);
-  void finalize_convergence(RunStats& st);
+  bool finalize_convergence(RunStats& st);  // true: it enqueued recompute launches
   double ipc_allreduce_residual();
   void* rccl_comm_ = nullptr;       // ncclComm_t
   int rccl_rank_ = 0, rccl_nranks_ = 1;

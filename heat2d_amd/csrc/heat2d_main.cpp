@@ -16,8 +16,15 @@
 #include <sys/stat.h>
 #include <vector>
 
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <signal.h>
+#include <sys/socket.h>
 #include <sys/wait.h>
 #include <unistd.h>
+
+#include <cerrno>
+#include <set>
 
 #include "bootstrap.h"
 #include "cpu_reference.h"
@@ -139,24 +146,33 @@ void write_outputs(Engine& e, Bootstrap& boot, const std::string& outdir, const 
   boot.barrier();
 }
 
-// `heat2d --np P ...`: the mpiexec of this program.  Forks P ranks BEFORE anything touches a
-// GPU (each child execs this binary with RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR set),
-// waits for all of them, and returns the first failure.
-int launch_ranks(int np, int argc, char** argv) {
-  std::vector<std::string> args;
-  for (int i = 0; i < argc; ++i) {
-    if (std::string(argv[i]) == "--np") {
-      ++i;
-      continue;
-    }
-    args.push_back(argv[i]);
+// `heat2d --np P ...`: the mpiexec of this program.  Binds the bootstrap's listening socket
+// (127.0.0.1, a free port: no collision with another job), then forks P ranks BEFORE anything
+// touches a GPU.  A child returns -1 and carries on in main() as its rank (RANK / WORLD_SIZE /
+// LOCAL_RANK / MASTER_ADDR set; rank 0 inherits the socket) — no exec.  The parent waits for
+// all of them; on the first failure it stops the others (SIGTERM) so none is left waiting in a
+// collective, and returns that failure.
+int launch_ranks(int np) {
+  const int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = 0;
+  inet_pton(AF_INET, "127.0.0.1", &sa.sin_addr);
+  socklen_t len = sizeof(sa);
+  if (lfd < 0 || ::bind(lfd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0 || ::listen(lfd, np) != 0 ||
+      ::getsockname(lfd, reinterpret_cast<sockaddr*>(&sa), &len) != 0) {
+    std::perror("heat2d: bootstrap socket");
+    return 1;
   }
-  const int port = 20000 + (int)(::getpid() % 20000);
-  std::vector<pid_t> kids;
+  const int port = ntohs(sa.sin_port);
+  std::fflush(stdout);
+  std::fflush(stderr);
+  std::set<pid_t> alive;
   for (int r = 0; r < np; ++r) {
     const pid_t pid = ::fork();
     if (pid < 0) {
       std::perror("heat2d: fork");
+      for (pid_t k : alive) ::kill(k, SIGTERM);
       return 1;
     }
     if (pid == 0) {
@@ -165,21 +181,26 @@ int launch_ranks(int np, int argc, char** argv) {
       ::setenv("WORLD_SIZE", std::to_string(np).c_str(), 1);
       ::setenv("MASTER_ADDR", "127.0.0.1", 1);
       ::setenv("HEAT2D_BOOT_PORT", std::to_string(port).c_str(), 1);
-      std::vector<char*> cargv;
-      for (auto& x : args) cargv.push_back(const_cast<char*>(x.c_str()));
-      cargv.push_back(nullptr);
-      ::execv("/proc/self/exe", cargv.data());
-      std::perror("heat2d: exec");
-      std::_Exit(127);
+      ::setenv("HEAT2D_BOOT_LISTEN_FD", std::to_string(lfd).c_str(), 1);
+      return -1;
     }
-    kids.push_back(pid);
+    alive.insert(pid);
   }
+  ::close(lfd);
   int rc = 0;
-  for (pid_t k : kids) {
+  while (!alive.empty()) {
     int st = 0;
-    ::waitpid(k, &st, 0);
+    const pid_t k = ::waitpid(-1, &st, 0);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      break;
+    }
+    if (!alive.erase(k)) continue;
     const int c = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
-    if (c != 0 && rc == 0) rc = c;
+    if (c != 0 && rc == 0) {
+      rc = c;
+      for (pid_t o : alive) ::kill(o, SIGTERM);
+    }
   }
   return rc;
 }
@@ -250,7 +271,10 @@ int main(int argc, char** argv) {
     a[k] = argv[++i];
   }
   if (a.count("help")) usage(nullptr);
-  if (a.count("np") && std::atoi(a["np"].c_str()) > 1) return launch_ranks(std::atoi(a["np"].c_str()), argc, argv);
+  if (a.count("np") && std::atoi(a["np"].c_str()) > 1) {
+    const int rc = launch_ranks(std::atoi(a["np"].c_str()));
+    if (rc >= 0) return rc;  // the launcher; a forked rank continues below
+  }
   const RankEnv env = rank_env();
   const int world = env.world;
   const std::string pname = a.count("preset") ? a["preset"] : "heat2d";
@@ -303,7 +327,9 @@ int main(int argc, char** argv) {
   if (world > 1) {
     o.ranks = {env.rank};
     if (dev != "gpu") o.transport = kTransportExternal;
-    else if ((tsel == "auto" || tsel == "ipc") && rows) o.transport = kTransportIpc;
+    // direct IPC needs halo units of at least max(K, G) rows at both ends of every strip
+    else if (tsel == "ipc" || (tsel == "auto" && rows && o.nx / o.gridx >= 2 * (int64_t)o.tblock))
+      o.transport = kTransportIpc;
     else o.transport = kTransportRccl;
   }
   const bool quiet = a.count("quiet") > 0 || env.rank != 0;
@@ -321,7 +347,23 @@ int main(int argc, char** argv) {
   try {
     Bootstrap boot(env.rank, world, env.addr, env.port);
     std::unique_ptr<ShmBarrier> shm = node_barrier(boot);
-    Engine e(o);
+    std::unique_ptr<Engine> ep;
+    std::string why;
+    try {
+      ep = std::make_unique<Engine>(o);
+    } catch (const std::exception& ex) {
+      why = ex.what();
+    }
+    // every rank agrees: an engine the automatic choice (direct IPC) cannot build on some rank
+    // falls back to RCCL together; a requested transport fails as requested
+    if (boot.allreduce_min(ep ? 1.0 : 0.0) < 0.5) {
+      if (!(o.transport == kTransportIpc && tsel == "auto"))
+        throw std::runtime_error(why.empty() ? "engine construction failed on another rank" : why);
+      ep.reset();
+      o.transport = kTransportRccl;
+      ep = std::make_unique<Engine>(o);
+    }
+    Engine& e = *ep;
     if (o.transport == kTransportIpc && e.has_exchange()) {
       e.ipc_open(boot.allgather(e.ipc_handle()));
       boot.barrier();

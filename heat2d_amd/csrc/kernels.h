@@ -140,6 +140,13 @@ struct StreamArgs {
   long long halo_polls = 0;
   unsigned int* timed_out = nullptr;
   unsigned int* timed_out_host = nullptr;  // host-mapped mirror of *timed_out (polled by the host per chunk)
+  // Observability (s_memrealtime, 100 MHz).  wait_acc (halo units of the direct / signalled
+  // pipelines): [0] += ticks spent in the halo wait, [1] += 1, [2] = max ticks — the exposed
+  // communication time, the analogue of the reference's MPI_Waitall share (Report.pdf p.34-37).
+  // stamps (diagnostics, usually null): per wave w, stamps[4w..4w+3] = {start, halo wait done,
+  // end, hardware id (XCC_ID << 16 | HW_ID[15:0])}.
+  unsigned long long* wait_acc = nullptr;
+  unsigned long long* stamps = nullptr;
 };
 
 // Largest K with a compiled streaming kernel.

@@ -19,6 +19,9 @@ struct ShmBarrier::Page {
   alignas(128) std::atomic<uint64_t> count;
   alignas(128) std::atomic<uint64_t> gen;
   alignas(128) std::atomic<uint64_t> world;
+  // set by a rank whose wait timed out: its arrival is still counted, so the generation count is
+  // off by one for good — every later wait (any rank) fails instead of releasing ranks early
+  alignas(128) std::atomic<uint64_t> broken;
 };
 static_assert(sizeof(std::atomic<uint64_t>) == 8 && std::atomic<uint64_t>::is_always_lock_free,
               "the barrier words must be lock-free 64-bit atomics (shared between processes)");
@@ -69,6 +72,8 @@ void ShmBarrier::unlink() {
 
 double ShmBarrier::wait(double timeout_s) {
   const auto t0 = std::chrono::steady_clock::now();
+  if (page_->broken.load(std::memory_order_acquire) != 0)
+    throw std::runtime_error("ShmBarrier: broken by an earlier timeout (discard it)");
   const uint64_t g = gen_;
   if (page_->count.fetch_add(1, std::memory_order_acq_rel) == (uint64_t)world_ - 1) {
     page_->count.store(0, std::memory_order_relaxed);  // nobody adds again before gen moves
@@ -81,9 +86,13 @@ double ShmBarrier::wait(double timeout_s) {
 #endif
       if ((++spins & 0xffff) == 0) {
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (el > timeout_s)
+        if (page_->broken.load(std::memory_order_acquire) != 0)
+          throw std::runtime_error("ShmBarrier: broken by another rank's timeout");
+        if (el > timeout_s) {
+          page_->broken.store(1, std::memory_order_release);
           throw std::runtime_error("ShmBarrier: rank " + std::to_string(rank_) + " timed out after " +
                                    std::to_string(el) + " s (a rank did not arrive)");
+        }
         // long waits (a rank still compiling / allocating): give the core back now and then
         if (el > 0.05) std::this_thread::yield();
       }

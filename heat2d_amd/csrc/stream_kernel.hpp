@@ -353,6 +353,8 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const int w = (int)blockIdx.x * 4 + wv;
   if (w >= a.nunits) return;
   const int lane = (int)(threadIdx.x & 63);
+  const bool stamping = a.stamps != nullptr;  // diagnostics: per-wave timeline
+  const unsigned long long t_start = stamping ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const Unit u = a.units[w];
   const bool halo_unit = w < a.nsignal;
   const int dir = (u.flags & kUnitReverse) ? 1 : 0;  // 0: north halo (top unit), 1: south (bottom unit)
@@ -367,6 +369,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     // wait until the exchange that fills this unit's ghost rows has landed (a wait that already
     // timed out in this engine stops every later wait: fail fast)
     if (lane == 0 && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       long long i = 0;
       // relaxed polls (an acquire per poll is 2-3x slower per hop), ONE acquire after the match
       while (__hip_atomic_load(a.wait[dir], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.need[dir]) {
@@ -376,6 +379,12 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
         }
         __builtin_amdgcn_s_sleep(2);
       }
+      if (a.wait_acc != nullptr) {  // exposed halo wait of this unit (fire-and-forget atomics)
+        const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+        __hip_atomic_fetch_add(a.wait_acc, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(a.wait_acc + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(a.wait_acc + 2, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     // acq 0: system scope; 1: agent scope (this CU's L1); 2: the ghost rows are in uncached
     // memory and were polled for: only keep the compiler from hoisting their loads
@@ -383,6 +392,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     else if (a.acq == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  const unsigned long long t_ready = stamping ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int64_t x0 = u.x0;
   const int h = u.h;
   const int64_t cb = (int64_t)u.cb + 4 * lane;
@@ -451,6 +461,19 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     int slot = w + a.prot;
     if (slot >= a.nunits) slot -= a.nunits;
     publish_partial(a.partials, slot, racc, a.nunits, a.dec, lane);
+  }
+  if (stamping) {
+    // the wave's stores have drained: its work is done, not just issued
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    const unsigned hw = (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 16) | (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xffffu);
+    if (lane == 0) {
+      unsigned long long* s = a.stamps + 4 * (int64_t)w;
+      s[0] = t_start;
+      s[1] = t_ready;
+      s[2] = t_end;
+      s[3] = hw;
+    }
   }
 }
 

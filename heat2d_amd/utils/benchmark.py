@@ -95,39 +95,45 @@ def parallelism_label(world: int, gx: int, gy: int) -> str:
     return f"rows{gx}" if gy == 1 else f"blocks{gx}x{gy}"
 
 
-# Engine keyword options of each halo pipeline (EngineOptions, engine.h).
+# Engine keyword options of each halo pipeline (EngineOptions, engine.h).  "direct-sys" is the
+# direct IPC pipeline with system-scope release before every flag bump and system-scope acquire
+# after every halo wait: the documented-safe fences, for when the measured default (no release:
+# the payload goes to the peer's uncached memory and is drained before the flag; agent acquire)
+# fails between distinct devices.
 PIPELINE_OPTIONS = {
     "auto": {},
+    "direct-sys": dict(direct_release=0, direct_acquire=0),
     "signal": dict(signal_exchange=2),
-    "concurrent": dict(signal_exchange=0, concurrent=1),
-    "boundary-first": dict(signal_exchange=0, concurrent=0),
     "serial": dict(overlap=False),
 }
 
 
 def candidates(transport: str, pipeline: str, world: int, on_gpu: bool, distinct_devices: bool,
-               layout: str) -> List[Tuple[str, str]]:
+               layout: str, rows_per_rank: int = 1 << 30, depth: int = 8) -> List[Tuple[str, str]]:
     """(transport, pipeline) pairs to try, in order: the requested one first, then the safer
-    fallbacks of the same family.  A run is only timed with a pair that passed the gate."""
+    fallbacks.  A run is only timed with a pair that passed the gate.  Between distinct devices
+    (never exercised on one GPU): direct IPC with the measured fences, direct IPC with
+    system-scope fences, RCCL (signalled, then serial), and host staging over gloo as the last
+    resort (no device-to-device path at all).  Direct IPC needs row strips of at least
+    2 * depth rows (halo units of at least `depth` rows at both ends of every column strip)."""
     if world == 1:
         return [("local", pipeline)]
     if not on_gpu:
         return [("torch", "serial")]
     rows = layout == "rows"
+    ipc_ok = rows and rows_per_rank >= 2 * depth
+    ipc = [("ipc", "auto"), ("ipc", "direct-sys")] if ipc_ok else []
     if not distinct_devices:  # several ranks per GPU: RCCL refuses them; IPC and gloo host staging work
-        if transport in ("auto", "ipc") and rows:
-            return [("ipc", "auto"), ("host", "serial")]
-        return [("host", "serial")]
+        chain = ipc if transport in ("auto", "ipc") else []
+        return chain + [("host", "serial")]
     chain: List[Tuple[str, str]] = []
-    if transport == "auto":
-        # 1-D row strips: direct peer stores over xGMI first (no RCCL kernel, no comm stream)
-        chain += [("ipc", "auto")] if rows else []
-        chain += [("rccl", pipeline), ("rccl", "boundary-first"), ("rccl", "serial"), ("torch", "serial")]
-    else:
+    if transport in ("auto", "ipc"):
+        chain += ipc
+    if transport in ("auto", "rccl"):
+        chain += [("rccl", "signal" if pipeline == "auto" else pipeline), ("rccl", "serial")]
+    elif transport not in ("ipc", "host"):
         chain += [(transport, pipeline)]
-        if transport == "rccl":
-            chain += [("rccl", "boundary-first"), ("rccl", "serial")]
-        chain += [("torch", "serial")]
+    chain += [("host", "serial")]
     out: List[Tuple[str, str]] = []
     for c in chain:
         if c not in out:
@@ -161,44 +167,72 @@ class GateResult:
 def gate_grid(world: int, gx: int, gy: int, G: int) -> Tuple[int, int, int]:
     """A small grid with the run's decomposition shape: several work units per column strip
     (so the halo units are the full-size signalling kind), three column strips, and a step
-    count with balanced and ragged chunks."""
+    count of a dozen chunks — both receive-buffer parities crossed several times — with
+    balanced and ragged chunks."""
     rows = max(6 * G, 48)
-    return rows * gx, 700 * gy, 5 * G + 3
+    return rows * gx, 700 * gy, 12 * G + 3
 
 
-def run_gate(ctx, make_solver: Callable[[str, str, int, int, int], object], oracle: Callable[[int, int, int], object],
-             cands: Sequence[Tuple[str, str]], gx: int, gy: int, G: int, log=print) -> GateResult:
-    """Try each (transport, pipeline) on a small grid of the same decomposition: gather the
-    final grid to rank 0 and compare it bit for bit with the CPU oracle.  Every rank takes part
-    in every attempt and all agree (min over ranks) before moving on."""
+def forced_failure(transport: str, pipeline: str) -> bool:
+    """Test hook: HEAT2D_GATE_FAIL="ipc,rccl/signal" makes those transports (any pipeline) or
+    transport/pipeline pairs fail the gate — rehearses the downgrade path on hardware where they
+    would pass."""
+    forced = {t for t in os.environ.get("HEAT2D_GATE_FAIL", "").split(",") if t}
+    return transport in forced or f"{transport}/{pipeline}" in forced
+
+
+def gate_one(ctx, make_solver, oracle, transport: str, pipeline: str, gx: int, gy: int, G: int) -> Tuple[int, str]:
+    """One candidate on the gate grid, twice: a plain run, then a run with a convergence check
+    every G+1 steps that never converges (sensitivity 0: the residual launches, the decision and
+    the cross-rank sum all run, the grid is the plain one).  Rank 0 compares the gathered grid
+    with the CPU oracle bit for bit.  Returns (ok on this rank, why not)."""
     import numpy as np
 
     nx, ny, steps = gate_grid(ctx.world, gx, gy, G)
-    tried = []
-    # test hook: HEAT2D_GATE_FAIL="ipc,rccl" makes those transports fail the gate (rehearses
-    # the downgrade path on hardware where they would pass)
-    forced = {t for t in os.environ.get("HEAT2D_GATE_FAIL", "").split(",") if t}
-    for transport, pipeline in cands:
-        ok, why = 1, ""
-        s = None
+    if forced_failure(transport, pipeline):
+        return 0, "failure injected by HEAT2D_GATE_FAIL"
+    agree = (lambda v: int(ctx.allreduce_min(v))) if hasattr(ctx, "allreduce_min") else (lambda v: v)
+    ref = None
+    for conv in (False, True):
+        ok, why, s = 1, "", None
         try:
-            if transport in forced:
-                raise RuntimeError("failure injected by HEAT2D_GATE_FAIL")
-            s = make_solver(transport, pipeline, nx, ny, steps)
+            s = make_solver(transport, pipeline, nx, ny, steps, conv=conv)
             s.run_steps(steps)
             s.engine.synchronize()
             full = s.gather()
             if ctx.rank == 0:
-                ref = oracle(nx, ny, steps)
+                ref = oracle(nx, ny, steps) if ref is None else ref
                 if not np.array_equal(full, ref):
-                    ok, why = 0, f"mismatch: {int(np.sum(full != ref))} cells differ"
+                    ok = 0
+                    why = f"mismatch{' (with convergence checks)' if conv else ''}: {int(np.sum(full != ref))} cells differ"
         except Exception as e:  # a failing transport must not take the job down: fall back
             ok, why = 0, f"{type(e).__name__}: {e}"
         finally:
             if s is not None:
                 s.close()
+        if not agree(ok):  # every rank leaves together (the next phase is collective)
+            return 0, why
+    return 1, ""
+
+
+def run_gate(ctx, make_solver: Callable[..., object], oracle: Callable[[int, int, int], object],
+             cands: Sequence[Tuple[str, str]], gx: int, gy: int, G: int, log=print,
+             accept: Optional[Callable[[str, str], Tuple[int, str]]] = None) -> GateResult:
+    """Try each (transport, pipeline) on a small grid of the same decomposition (gate_one).
+    Every rank takes part in every attempt and all agree (min over ranks) before moving on.
+    `accept` (optional, collective) is a second test of a candidate that passed: e.g. building
+    the timed solver and verifying its first steps; a refusal moves on to the next candidate."""
+    tried = []
+    for transport, pipeline in cands:
+        ok, why = gate_one(ctx, make_solver, oracle, transport, pipeline, gx, gy, G)
         ok_all = int(ctx.allreduce_min(ok)) if hasattr(ctx, "allreduce_min") else ok
-        tried.append({"transport": transport, "pipeline": pipeline, "ok": bool(ok_all), "detail": why})
+        if ok_all and accept is not None:
+            ok, why = accept(transport, pipeline)
+            ok_all = int(ctx.allreduce_min(ok)) if hasattr(ctx, "allreduce_min") else ok
+            if not ok_all and not why:
+                why = "refused on another rank"
+        rec = {"transport": transport, "pipeline": pipeline, "ok": bool(ok_all), "detail": why}
+        tried.append(rec)
         if ok_all:
             return GateResult(True, transport, pipeline, why, tried)
         if why:

@@ -48,10 +48,24 @@ def test_tile_bytes_matches_engine_geometry(native):
 def test_candidate_chains():
     assert B.candidates("auto", "auto", 1, True, True, "rows") == [("local", "auto")]
     assert B.candidates("auto", "auto", 4, False, False, "rows") == [("torch", "serial")]
-    assert B.candidates("auto", "auto", 2, True, False, "rows") == [("ipc", "auto"), ("host", "serial")]
+    # ranks sharing one GPU: both direct flavours, then host staging
+    assert B.candidates("auto", "auto", 2, True, False, "rows") == [("ipc", "auto"), ("ipc", "direct-sys"),
+                                                                    ("host", "serial")]
     assert B.candidates("auto", "auto", 2, True, False, "blocks") == [("host", "serial")]
+    # distinct devices (the first cross-device run must fail safe): measured fences, system-scope
+    # fences, RCCL signalled, RCCL serial, host staging
     ch = B.candidates("auto", "auto", 8, True, True, "rows")
-    assert ch[0] == ("ipc", "auto") and ch[1] == ("rccl", "auto") and ch[-1] == ("torch", "serial")
-    assert ("rccl", "serial") in ch
-    assert B.candidates("auto", "auto", 8, True, True, "blocks")[0] == ("rccl", "auto")
+    assert ch == [("ipc", "auto"), ("ipc", "direct-sys"), ("rccl", "signal"), ("rccl", "serial"), ("host", "serial")]
+    assert B.candidates("auto", "auto", 8, True, True, "blocks") == [("rccl", "signal"), ("rccl", "serial"),
+                                                                     ("host", "serial")]
+    # strips too short for halo units of the depth: no direct IPC candidate
+    assert B.candidates("auto", "auto", 8, True, True, "rows", rows_per_rank=10, depth=7)[0] == ("rccl", "signal")
+    assert B.candidates("rccl", "serial", 8, True, True, "rows") == [("rccl", "serial"), ("host", "serial")]
     assert len(ch) == len(set(ch))
+
+
+def test_forced_gate_failures(monkeypatch):
+    monkeypatch.setenv("HEAT2D_GATE_FAIL", "ipc/auto,rccl")
+    assert B.forced_failure("ipc", "auto") and not B.forced_failure("ipc", "direct-sys")
+    assert B.forced_failure("rccl", "signal") and B.forced_failure("rccl", "serial")
+    assert not B.forced_failure("host", "serial")

@@ -42,6 +42,46 @@ def test_every_compiled_K(native, gpu, K):
         assert np.array_equal(eng.download(0), ref), (K, boundary)
 
 
+def test_bench_shape_4096_k7_writethrough(native, gpu):
+    """Exactly the timed configuration of the headline bench: 4096^2, depth 7, write-through
+    output stores, 20 steps = 7+7+6, capacity-fitted units (~1000, h ~ 68) — against the oracle."""
+    eng = native.Engine(4096, 4096, tblock=7, device=gpu, small_grid_lds=False, tiled=0, wt_store=1)
+    st = eng.run(20)
+    assert st["path"] == "stream" and st["steps_done"] == 20 and st["chunks"] == 3
+    assert eng.num_units(7) > 900
+    assert np.array_equal(eng.download(0), oracle(native, 4096, 4096, 20)["grid"])
+
+
+@pytest.mark.parametrize("rows,K", [(512, 6), (1024, 7)])
+def test_strong_scaling_rank_tiles_direct(native, gpu, rows, K):
+    """The per-rank tiles of 4096^2 over 8 and 4 GPUs, row-periodic through the direct IPC
+    pipeline (the rank is its own neighbour): bit-exact, and the halo-wait counters see every
+    halo unit's wait."""
+    steps = 3 * K + 2
+    e = native.Engine(rows, 4096, periodic_x=True, tblock=K, device=gpu, ranks=[0], transport=native.TRANSPORT_IPC,
+                      halo_timeout_s=5.0)
+    e.ipc_open([e.ipc_handle()])
+    e.ipc_prime()
+    e.reset_halo_wait()
+    st = e.run(steps)
+    assert st["steps_done"] == steps
+    ref = oracle(native, rows, 4096, steps, per=(True, False))["grid"]
+    assert np.array_equal(e.download(0), ref)
+    hw = e.halo_wait()
+    halo_units = sum(1 for u in e.unit_list(0, K, 3) if u[3] & 4) * 2  # top + bottom units per strip
+    assert hw["waits"] >= halo_units and hw["max_us"] >= 0.0 and hw["total_us"] >= 0.0
+
+
+def test_timeline_stamps(native, gpu):
+    e = native.Engine(256, 4096, tblock=6, device=gpu, small_grid_lds=False, tiled=0, timeline=8)
+    e.run(12)
+    tl = e.timeline()
+    assert [k for k, _ in tl] == [6, 6]
+    for _k, st in tl:
+        assert st.shape[1] == 4 and (st[:, 2] >= st[:, 1]).all() and (st[:, 1] >= st[:, 0]).all()
+    assert tl[1][1][:, 0].min() >= tl[0][1][:, 2].min()  # the second launch starts after the first's waves
+
+
 @pytest.mark.parametrize("H", [1, 5, 16, 64, 300])
 def test_rows_per_wave_variants(native, gpu, H):
     nx, ny, steps = 150, 300, 17

@@ -143,8 +143,19 @@ def test_bench_weak_and_blocks_cpu_rehearsal(tmp_path):
     d = _bench(4, ["--gpus", "4", "--steps", "5", "--warmup", "1", "--config", "weak-4096", "--side", "40",
                    "--layout", "blocks", "--device", "cpu"], tmp_path)
     assert d["scaling"] == "weak" and d["config"]["grid"] == [80, 80] and d["config"]["grid_per_gpu"] == [40, 40]
-    assert d["config"]["parallelism"] == "blocks2x2" and d["verified"] is None
+    assert d["config"]["parallelism"] == "blocks2x2"
+    # the timed solver's first 5 steps were checked against the CPU oracle on the whole 80x80 grid
+    assert d["verified"] is True and "CPU oracle" in d["verification"]
     assert abs(d["speedup"] - 4 * d["efficiency"]) < 1e-12
+
+
+def test_bench_weak_hbm_efficiency_cpu_rehearsal(tmp_path):
+    """weak-hbm at N=4: the single-rank reference tile is timed before the N-rank solver
+    allocates (on a GPU both would not fit), so speedup and efficiency are reported."""
+    d = _bench(4, ["--gpus", "4", "--steps", "4", "--warmup", "1", "--config", "weak-hbm", "--device", "cpu"], tmp_path)
+    assert d["scaling"] == "weak" and d["config"]["grid_per_gpu"] == [64, 64]
+    assert d["efficiency"] is not None and d["efficiency"] > 0 and abs(d["speedup"] - 4 * d["efficiency"]) < 1e-12
+    assert "before the N-rank solver" in d["speedup_reference"]
 
 
 def test_bench_gate_all_candidates_fail_cpu(tmp_path):

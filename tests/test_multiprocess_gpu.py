@@ -79,19 +79,34 @@ def test_gpu_bench_two_ranks_ipc(tmp_path):
     lines = [l for l in out.splitlines() if l.startswith("{")]
     d = json.loads(lines[-1])
     assert d["config"]["transport"] == "ipc" and d["config"]["pipeline"] == "direct"
-    assert d["gate"][0]["ok"] and d["verified"] is True
+    assert d["gate"][0]["ok"] and d["verified"] is True and "CPU oracle" in d["verification"]
+    hw = d["halo_wait"]
+    assert min(hw["waits_per_rank"]) > 0 and 0.0 <= hw["share_of_chunk"] and hw["max_us"] >= hw["mean_us_per_halo_unit"]
 
 
 def test_gpu_bench_two_ranks_gate_downgrade(tmp_path, monkeypatch):
-    """The first candidate (direct IPC) fails the gate (injected): every rank falls back to the
-    next one together, the run is timed with it and the JSON says what failed."""
-    monkeypatch.setenv("HEAT2D_GATE_FAIL", "ipc")
+    """Both direct IPC flavours fail the gate (injected per transport/pipeline): every rank falls
+    back together to the third candidate, the run is timed with it, verified, and the JSON says
+    what failed and which candidate was used."""
+    monkeypatch.setenv("HEAT2D_GATE_FAIL", "ipc/auto,ipc/direct-sys")
     out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5", "--side",
                         "512", "--prewarm-s", "0"], str(tmp_path))
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
-    assert d["gate"][0]["transport"] == "ipc" and not d["gate"][0]["ok"]
-    assert d["gate"][1]["ok"] and d["config"]["transport"] == d["gate"][1]["transport"] == "host"
+    assert [(g["transport"], g["pipeline"], g["ok"]) for g in d["gate"]] == [
+        ("ipc", "auto", False), ("ipc", "direct-sys", False), ("host", "serial", True)]
+    assert d["config"]["transport"] == "host" and d["config"]["candidate"] == "host/serial"
     assert d["verified"] is True
+
+
+def test_gpu_bench_two_ranks_direct_sys(tmp_path, monkeypatch):
+    """Only the measured-fence flavour fails: the system-scope-fence direct pipeline is timed."""
+    monkeypatch.setenv("HEAT2D_GATE_FAIL", "ipc/auto")
+    out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5", "--side",
+                        "512", "--prewarm-s", "0"], str(tmp_path))
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert not d["gate"][0]["ok"] and d["gate"][1]["ok"]
+    assert d["config"]["candidate"] == "ipc/direct-sys" and d["config"]["pipeline"] == "direct"
+    assert d["verified"] is True and d["halo_wait"]["waits_per_rank"][0] > 0
 
 
 def test_gpu_bench_two_ranks_host_transport(tmp_path):

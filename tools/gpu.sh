@@ -1,0 +1,42 @@
+#!/bin/bash
+# One parameterised driver for GPU-box work (run under gpurun from the repo root):
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- 'bash tools/gpu.sh tests smoke bench20 timeline'
+# Every step runs under its own time limit and writes under gpurun_out/; the first failing step
+# ends the script (no GPU step runs after a fault, abort or time-out).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export HEAT2D_NO_BUILD=1 TMPDIR=/tmp
+
+step() {  # step NAME SECONDS CMD...: run, log, stop the script on failure
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -n 3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ]; then
+    echo "== $name FAILED rc=$rc"
+    exit $rc
+  fi
+}
+
+for s in "$@"; do
+  case "$s" in
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    tests-new) step tests-new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+                 tests/test_gpu_engine.py -k "bench_shape or rank_tiles or timeline" ;;
+    mp) step mp 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_multiprocess_gpu.py ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;
+    bench1000) step bench1000 300 python bench.py --steps 1000 --warmup 200 ;;
+    timeline) step timeline 300 python -u tools/timeline.py 4096x4096:7:20 4096x4096:7:70 2048x4096:7:70 \
+                1024x4096:7:70 512x4096:6:60 512x4096:6:60:direct 1024x4096:7:70:direct \
+                --json gpurun_out/timeline.json ;;
+    proxy) step proxy 600 python -u tools/strong_proxy.py 4096 840 6,7,8 0 '' 1,2,4,8 ;;
+    prof) step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
+            python bench.py --steps 20 --warmup 5 --repeat 3 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== all done ($(date +%T))"
