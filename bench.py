@@ -230,7 +230,7 @@ def main() -> int:
 
     rows_per_rank = nx // gx
     cands = B.candidates(a.transport, a.pipeline, world, on_gpu, ctx.distinct_devices, layout,
-                         rows_per_rank=rows_per_rank, depth=a.tblock)
+                         rows_per_rank=rows_per_rank, depth=a.tblock, cols_per_rank=ny // gy)
     gate = None
     log = lambda m: print(m, file=sys.stderr, flush=True)  # noqa: E731
     if world > 1 and not a.no_gate:

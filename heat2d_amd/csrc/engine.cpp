@@ -114,8 +114,16 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
   if (transport_ == kTransportRccl && !on_gpu()) throw std::invalid_argument("RCCL transport needs a GPU");
   if (transport_ == kTransportIpc) {
     if (ranks.size() != 1 || !on_gpu()) throw std::invalid_argument("IPC transport: one tile per process, on a GPU");
-    if (o.gridy != 1 || o.periodic_y)
-      throw std::invalid_argument("IPC transport: 1-D row strips only (gridy == 1, not periodic in y)");
+    bool side = false;
+    for (int d = kW; d < kNumDirs; ++d) side = side || dec_.neighbor(ranks[0], d) >= 0;
+    if (side) {
+      // 2-D blocks: W / E ghost columns are whole lanes of the streaming kernel (4 columns each)
+      const TileGeom g0 = dec_.tile(ranks[0], G_);
+      if (g0.ycell % 4 != 0 || g0.ycell < 2 * kGhostGroup)
+        throw std::invalid_argument("IPC transport with west/east neighbours: the tile width (" +
+                                    std::to_string(g0.ycell) + ") must be a multiple of 4 and at least " +
+                                    std::to_string(2 * kGhostGroup));
+    }
   }
   direct_ = transport_ == kTransportIpc && has_exchange_;
 
@@ -257,48 +265,11 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
         H2D_HIP_CHECK(hipMemset(halo_counter_, 0, sizeof(unsigned long long)));
       }
     }
-    // Overlap mode: run the halo-dependent boundary units CONCURRENTLY with the interior
-    // (second stream) when they are few — e.g. 1-D row decompositions — otherwise first.
-    concurrent_ = false;
-    if (has_exchange_ && opt_.overlap && opt_.concurrent != 0 && sig_mode_ == 0 && !direct_) {
-      if (opt_.concurrent > 0) {
-        concurrent_ = true;
-      } else {
-        int64_t nb = 0;
-        for (int t = 0; t < (int)tiles_.size(); ++t) nb += units(t, G_).n_boundary;
-        concurrent_ = nb * 8 <= wave_capacity(G_);
-        for (auto& kv : units_) {
-          hipFree(kv.second.d_all);
-          hipFree(kv.second.d_interior);
-          hipFree(kv.second.d_boundary);
-          hipFree(kv.second.d_bfirst);
-        }
-        units_.clear();
-      }
-    }
-    if (concurrent_) {
-      if (comm_cus_ > 0) {
-        std::vector<uint32_t> m(4096 / 32);
-        H2D_HIP_CHECK(hipExtStreamGetCUMask(compute_, (uint32_t)m.size(), m.data()));
-        H2D_HIP_CHECK(hipExtStreamCreateWithCUMask(&bstream_, (uint32_t)m.size(), m.data()));
-      } else {
-        H2D_HIP_CHECK(hipStreamCreateWithFlags(&bstream_, hipStreamNonBlocking));
-      }
-      for (int i = 0; i < 2; ++i) {
-        const unsigned evf = hipEventDisableTiming | (o.device_fence_events ? hipEventDisableSystemFence : 0u);
-        H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_i_[i], evf));
-        H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_b_[i], evf));
-      }
-    }
+    // every unit list up front (a direct plan that cannot be built fails here, before any
+    // bootstrap collective)
     for (int t = 0; t < (int)tiles_.size(); ++t)
       for (int K = 1; K <= G_; ++K)
-        if (stream_k_supported(K)) {
-          const UnitLists& L = units(t, K);
-          if (direct_ && L.sig_rows <= 0)
-            throw std::invalid_argument("IPC transport: the tile is too short for full-size halo units (" +
-                                        std::to_string(tiles_[t].g.xcell) + " rows, halo depth " +
-                                        std::to_string(G_) + ")");
-        }
+        if (stream_k_supported(K)) (void)units(t, K);
     // LDS-tiled path: one tile owning the whole grid (any periodic halo is its own wrap).
     const bool self_only = tiles_.size() == 1 && transport_ == kTransportLocal;
     if (self_only && !opt_.naive && opt_.tiled != 0) {
@@ -409,11 +380,6 @@ Engine::~Engine() {
   hipEventDestroy(ev_done_);
   for (auto& e : ev_prog_)
     if (e) hipEventDestroy(e);
-  if (bstream_) hipStreamDestroy(bstream_);
-  for (int i = 0; i < 2; ++i) {
-    if (ev_i_[i]) hipEventDestroy(ev_i_[i]);
-    if (ev_b_[i]) hipEventDestroy(ev_b_[i]);
-  }
   hipStreamDestroy(compute_);
   hipStreamDestroy(comm_);
 }
@@ -458,37 +424,41 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   const int hb = std::max(opt_.boundary_rows, G_);
   UnitPlan P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                           opt_.edge_weight, cap, peer, hb, opt_.row_edge_weight);
-  // auto headroom (4096^2 row-periodic RCCL self-exchange, us/step: 14.3 -> 10.4-10.9 with
-  // 16 in the concurrent pipeline; 14.3 -> 12.6 with 32 in the boundary-first one)
-  const int64_t reserve = opt_.reserve_waves >= 0 ? opt_.reserve_waves : ((concurrent_ || sig_mode_ > 0) ? 16 : 32);
-  if (!direct_ && has_exchange_ && opt_.overlap && !P.boundary.empty() && (concurrent_ || sig_mode_ > 0 || reserve > 0)) {
-    // interior units leave room for what runs beside them: the boundary units (concurrent
-    // and signalled pipelines) and the exchange kernels
-    const int64_t nb = (concurrent_ || sig_mode_ > 0) ? (int64_t)P.boundary.size() : 0;
+  // auto headroom: 16 wave slots (4096^2 row-periodic RCCL self-exchange, round 1: 14.3 ->
+  // 10.4-10.9 us/step with 16 slots kept free for the exchange kernels)
+  const int64_t reserve = opt_.reserve_waves >= 0 ? opt_.reserve_waves : 16;
+  if (!direct_ && has_exchange_ && sig_mode_ > 0 && !P.boundary.empty()) {
+    // interior units leave room for what runs beside them: the boundary units and the exchange
+    // kernels of the signalled pipeline
+    const int64_t nb = (int64_t)P.boundary.size();
     const int64_t cap_in = std::max<int64_t>(cap / 2, cap - nb - reserve);
     P = plan_units(g, K, opt_.rows_per_wave, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                    opt_.edge_weight, cap_in, peer, hb, opt_.row_edge_weight);
   }
-  // Signalled pipeline with only north/south peers (1-D row strips): no short boundary units.
-  // Every strip is cut into capacity-fitted units as if the tile had no peers; the top unit
-  // of a strip with a north peer and the bottom unit (streamed bottom-up) of a strip with a
-  // south peer become the signalling units: they wait for the halo, signal after their
-  // first K rows (the rows the exchange sends) and carry on with the rest of their rows.
-  // So the exchange starts early and no wave idles (the short-unit plan left nb waves idle
-  // for most of the launch and shrank the interior).
+  // Signalled pipeline with only north/south peers (1-D row strips), and the direct (IPC)
+  // pipeline for any decomposition: no short boundary units.  Every strip is cut into
+  // capacity-fitted units as if the tile had no peers; the top unit of a strip with a north
+  // peer and the bottom unit (streamed bottom-up) of a strip with a south peer become the N/S
+  // halo units (kUnitNS): they wait for the halo, signal after their first G rows (the rows the
+  // exchange sends) and carry on with the rest of their rows.  So the exchange starts early and
+  // no wave idles (the short-unit plan left nb waves idle for most of the launch).
+  // Direct pipeline with W/E / corner peers (2-D blocks): every unit of a strip whose outputs
+  // reach the first / last G columns also pushes them to the W / E neighbour (and the strip's
+  // top / bottom unit its G x G corner to the diagonal one), signalling at its end; it waits for
+  // the same neighbours' previous pushes first (Unit::links: waits == pushes, a superset of the
+  // ghost sides its cone reads, so a push never overtakes the neighbour's reads of the buffer
+  // parity it overwrites).
   L.sig_rows = 0;
   const bool ns_only = !peer[kW] && !peer[kE] && !peer[kNW] && !peer[kNE] && !peer[kSW] && !peer[kSE];
-  // The direct (IPC) pipeline uses the same plan; nothing runs beside its launches, so it
-  // keeps no wave slots in reserve.
-  if (((sig_mode_ > 0 && opt_.overlap && opt_.signal_plan != 0) || direct_) && has_exchange_ && ns_only &&
-      (peer[kN] || peer[kS])) {
+  const bool sig_plan = sig_mode_ > 0 && opt_.overlap && opt_.signal_plan != 0 && ns_only && (peer[kN] || peer[kS]);
+  if (has_exchange_ && (sig_plan || direct_)) {
+    // The direct pipeline keeps no wave slots in reserve: nothing runs beside its launches.
     const int64_t reserve_sig = direct_ ? 0 : opt_.reserve_waves >= 0 ? opt_.reserve_waves : 16;
-    // First the capacity-fitted plan; if its strip-end units are too short to be halo units,
-    // retry with units of at least 2*max(K, G) rows (fewer, taller units).
+    const int hmin = std::max(K, G_);  // a N/S halo unit owns every row the next exchange sends
     // Attempts: the capacity-fitted plan; the same without shortening edge-strip units (their
     // strip-end units may fall below G rows); units of at least 2*max(K, G) rows.
     for (int attempt = 0; attempt < 3 && L.sig_rows == 0; ++attempt) {
-    const int Hq = attempt < 2 ? opt_.rows_per_wave : std::max(opt_.rows_per_wave, 2 * std::max(K, G_));
+    const int Hq = attempt < 2 ? opt_.rows_per_wave : std::max(opt_.rows_per_wave, 2 * hmin);
     const double ew = attempt == 0 ? opt_.edge_weight : 1.0;
     if (attempt == 1 && ew == opt_.edge_weight) continue;
     if (attempt == 2 && Hq == opt_.rows_per_wave) break;
@@ -508,24 +478,45 @@ const Engine::UnitLists& Engine::units(int t, int K) {
       const int ti = kv.second.first, bi = kv.second.second;
       if (ti == bi) {
         if (peer[kN] || peer[kS]) role[ti] = 3;
-        if (direct_) ok = false;  // one unit would need both halos and push both ways
+        if (direct_ && (peer[kN] || peer[kS])) ok = false;  // one unit would need both halos and push both ways
         continue;
       }
       if (peer[kN]) role[ti] = 1;
       if (peer[kS]) role[bi] = 2;
       // the neighbouring units' K-cones must not reach the ghost rows, and a signalling unit
       // must own every row the next exchange sends (up to G_, whatever this chunk's K)
-      if ((peer[kN] && Q.interior[ti].h < std::max(K, G_)) || (peer[kS] && Q.interior[bi].h < std::max(K, G_)))
-        ok = false;
+      if ((peer[kN] && Q.interior[ti].h < hmin) || (peer[kS] && Q.interior[bi].h < hmin)) ok = false;
+    }
+    // side links of the direct pipeline
+    std::vector<int> links(Q.interior.size(), 0);
+    if (direct_ && !ns_only) {
+      for (int i = 0; i < (int)Q.interior.size(); ++i) {
+        const Unit& u = Q.interior[i];
+        const bool pw = u.olo < G_, pe = u.ohi > g.ycell - G_;  // outputs in the first / last G columns
+        const auto& e = ends.at(u.strip);
+        int pu = 0;
+        if (pw && peer[kW]) pu |= kLinkW;
+        if (pe && peer[kE]) pu |= kLinkE;
+        if (i == e.first && pw && peer[kNW]) pu |= kLinkNW;
+        if (i == e.first && pe && peer[kNE]) pu |= kLinkNE;
+        if (i == e.second && pw && peer[kSW]) pu |= kLinkSW;
+        if (i == e.second && pe && peer[kSE]) pu |= kLinkSE;
+        if (pu != 0 && (u.flags & kEdgeCols) != 0)
+          throw std::invalid_argument("direct transport: a " + std::to_string(g.ycell) +
+                                      "-column tile is too narrow (a side-pushing strip meets a global edge column)");
+        links[i] = pu | (pu << 8);
+      }
     }
     if (ok) {
       std::vector<Unit> sg, rest;
       for (int i = 0; i < (int)Q.interior.size(); ++i) {
         Unit u = Q.interior[i];
-        if (role[i] == 0) {
+        u.links = links[i];
+        if (role[i] == 0 && links[i] == 0) {
           rest.push_back(u);
           continue;
         }
+        if (role[i] != 0) u.flags |= kUnitNS;
         if (role[i] == 2) u.flags |= kUnitReverse;
         if (role[i] == 3) u.flags |= kUnitSigEnd;
         sg.push_back(u);
@@ -535,7 +526,12 @@ const Engine::UnitLists& Engine::units(int t, int K) {
       L.sig_rows = G_;  // released rows cover the deepest exchange that can follow
     }
     }
+    if (direct_ && L.sig_rows <= 0)
+      throw std::invalid_argument("IPC transport: the tile is too short for full-size halo units (" +
+                                  std::to_string(g.xcell) + " rows, halo depth " + std::to_string(G_) + ")");
   }
+  if (!direct_ && L.sig_rows == 0)
+    for (Unit& u : P.boundary) u.flags |= kUnitNS;  // short boundary units: all wait / signal
   std::vector<Unit>& in = P.interior;
   std::vector<Unit>& bd = P.boundary;
   std::vector<Unit> all = in;
@@ -543,7 +539,15 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   if (all.size() > (size_t)(1 << 30)) throw std::runtime_error("too many work units");
   L.H = 0;
   for (const Unit& u : in) L.H = std::max(L.H, u.h);
-  for (const Unit& u : bd) ++L.n_dir[(u.flags & kUnitReverse) ? 1 : 0];
+  for (const Unit& u : bd) {
+    if (u.flags & kUnitNS) {
+      const int d = (u.flags & kUnitReverse) ? 1 : 0;
+      ++L.n_dir[d];
+      ++L.pushes[d];  // kN / kS
+    }
+    for (int i = 0; i < kSideLinks; ++i)
+      if ((u.links >> (8 + i)) & 1) ++L.pushes[kW + i];
+  }
   L.n_all = (int)all.size();
   L.n_interior = (int)in.size();
   L.n_boundary = (int)bd.size();
@@ -636,21 +640,40 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
       const int p = (int)(ipc_chunk_ & 1), q = p ^ 1;
       const int pn = dec_.neighbor(tl.rank, kN), ps = dec_.neighbor(tl.rank, kS);
       const int64_t rowb = g.pitch * (int64_t)sizeof(float);
+      const IpcLayout& me = ipc_lays_[tl.rank];
       if (pn >= 0) {
-        a.wait[0] = reinterpret_cast<const unsigned long long*>(ipc_block_ + ipc_lay_.flag_n);
-        a.need[0] = ipc_need_[0];
-        a.hsrc[0] = reinterpret_cast<const float*>(ipc_block_ + ipc_lay_.recv_n[p]);  // rows -G..-1
-        a.push[0] = reinterpret_cast<float*>(ipc_blocks_[pn] + ipc_lay_.recv_s[q]);     // N's rows xcell.. = my 0..
-        a.sig[0] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pn] + ipc_lay_.flag_s);
+        const IpcLayout& nl = ipc_lays_[pn];
+        a.wait[0] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kN]);
+        a.need[0] = ipc_need_[kN];
+        a.hsrc[0] = reinterpret_cast<const float*>(ipc_block_ + me.recv_n[p]);  // rows -G..-1
+        a.push[0] = reinterpret_cast<float*>(ipc_blocks_[pn] + nl.recv_s[q]);   // N's rows xcell.. = my 0..
+        a.sig[0] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pn] + nl.flag[kS]);
       }
       if (ps >= 0) {
-        a.wait[1] = reinterpret_cast<const unsigned long long*>(ipc_block_ + ipc_lay_.flag_s);
-        a.need[1] = ipc_need_[1];
+        const IpcLayout& sl = ipc_lays_[ps];
+        a.wait[1] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kS]);
+        a.need[1] = ipc_need_[kS];
         // ghost row i (xcell <= i < xcell+G) is receive row i - xcell
-        a.hsrc[1] = reinterpret_cast<const float*>(ipc_block_ + ipc_lay_.recv_s[p] - (g.G + g.xcell) * rowb);
+        a.hsrc[1] = reinterpret_cast<const float*>(ipc_block_ + me.recv_s[p] - (g.G + g.xcell) * rowb);
         // my row i (xcell-G <= i < xcell) is S's ghost row i - xcell, its receive row i - xcell + G
-        a.push[1] = reinterpret_cast<float*>(ipc_blocks_[ps] + ipc_lay_.recv_n[q] - (g.xcell - g.G) * rowb);
-        a.sig[1] = reinterpret_cast<unsigned long long*>(ipc_blocks_[ps] + ipc_lay_.flag_n);
+        // (S has my pitch: the same block column)
+        a.push[1] = reinterpret_cast<float*>(ipc_blocks_[ps] + sl.recv_n[q] - (g.xcell - g.G) * rowb);
+        a.sig[1] = reinterpret_cast<unsigned long long*>(ipc_blocks_[ps] + sl.flag[kN]);
+      }
+      // 2-D blocks: W / E ghost-column groups (reads: mine of parity p; pushes: the neighbours'
+      // of parity q) and the corners
+      if (me.xbuf != 0) {
+        a.gsrc[0] = reinterpret_cast<const float*>(ipc_block_ + me.group(0, p));
+        a.gsrc[1] = reinterpret_cast<const float*>(ipc_block_ + me.group(1, p));
+      }
+      for (int i = 0; i < kSideLinks; ++i) {
+        const int d = kW + i, pr = dec_.neighbor(tl.rank, d);
+        if (pr < 0) continue;
+        a.xwait[i] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[d]);
+        a.xneed[i] = ipc_need_[d];
+        a.xsig[i] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pr] + ipc_lays_[pr].flag[kDirOpp[d]]);
+        a.xpush[i] = side_push_base(d, pr, q);
+        a.xpitch[i] = ipc_lays_[pr].pitch;
       }
       // Defaults (tools/direct_fence_probe.py, MI355X): the push goes to the peer's UNCACHED
       // block, so the acknowledged stores (vmcnt(0)) are complete and need no L2 write-back
@@ -891,8 +914,7 @@ std::string Engine::pipeline() const {
   if (direct_) return "direct";
   if (transport_ == kTransportExternal) return "external";
   if (sig_mode_ > 0) return "signal";
-  if (concurrent_) return opt_.comm_boundary != 0 ? "concurrent" : "concurrent3";
-  return opt_.overlap ? "boundary-first" : "serial";
+  return "serial";
 }
 
 void Engine::advance(int k, bool residual) {
@@ -1166,9 +1188,10 @@ RunStats Engine::run_impl(int64_t steps) {
         trace_begin("chunk", compute_);
         launch_chunk_tile(0, k, check, 3);
         trace_end("chunk", compute_);
-        const UnitLists& L = units(0, k);
-        ipc_need_[0] += (unsigned long long)L.n_dir[0];
-        ipc_need_[1] += (unsigned long long)L.n_dir[1];
+        for (int d = 0; d < kNumDirs; ++d) {  // the neighbours' pushes this chunk, for my next one
+          const int pr = dec_.neighbor(tiles_[0].rank, d);
+          if (pr >= 0) ipc_need_[d] += (unsigned long long)ipc_counts_[pr].at((size_t)k * kNumDirs + kDirOpp[d]);
+        }
         ++ipc_chunk_;
         tiles_[0].cur = 1 - tiles_[0].cur;
         ++st.chunks;
@@ -1250,199 +1273,6 @@ RunStats Engine::run_impl(int64_t steps) {
       }
       H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
       H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
-    } else if (has_exchange_ && concurrent_ && !opt_.naive && opt_.comm_boundary != 0) {
-      // Two-stream concurrent pipeline (per chunk c):
-      //   compute (I): wait evB[c-1] -> interior units(c) -> evI[c]
-      //   comm    (C): wait evI[c-1] -> boundary units(c) -> evB[c] -> halo exchange of chunk c+1
-      // The boundary units and the exchange that consumes their outputs share one stream, so
-      // the boundary -> exchange -> boundary cycle has no cross-queue wait in it (each
-      // cross-queue hand-off costs ~10-20 us of dispatch latency on gfx950, measured in
-      // profiles/overlap_trace_*.txt).  The interior is enqueued first so that a host-side
-      // RCCL enqueue stall never delays it.
-      bool check = false;
-      int k = next_chunk(steps_done_, target, &check);
-      H2D_HIP_CHECK(hipEventRecord(ev_i_[1], compute_));
-      H2D_HIP_CHECK(hipEventRecord(ev_b_[1], compute_));
-      if (k > 0) {
-        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_i_[1], 0));
-        trace_begin("exchange", comm_);
-        do_exchange_async(k);
-        trace_end("exchange", comm_);
-        ++st.exchanges;
-      }
-      int c = 0;
-      while (k > 0) {
-        const int p = c & 1, q = p ^ 1;
-        const int src = tiles_[0].cur;
-        H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[q], 0));
-        trace_begin("interior", compute_);
-        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1, src, compute_);
-        trace_end("interior", compute_);
-        H2D_HIP_CHECK(hipEventRecord(ev_i_[p], compute_));
-        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_i_[q], 0));
-        trace_begin("boundary", comm_);
-        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2, src, comm_);
-        trace_end("boundary", comm_);
-        H2D_HIP_CHECK(hipEventRecord(ev_b_[p], comm_));
-        for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
-        ++st.chunks;
-        bool check_next = false;
-        const int k_next = next_chunk(steps_done_ + k, target, &check_next);
-        if (check) {
-          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[p], 0));
-          for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
-          if (fused_) {
-            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
-          } else {
-            st.residual = finish_residual();
-            if (st.residual < opt_.sensitivity) {
-              rollback();
-              st.converged = true;
-              break;
-            }
-          }
-        }
-        if (k_next > 0) {
-          trace_begin("exchange", comm_);
-          do_exchange_async(k_next);
-          trace_end("exchange", comm_);
-          ++st.exchanges;
-        }
-        steps_done_ += k;
-        k = k_next;
-        check = check_next;
-        ++c;
-      }
-      H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
-      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
-    } else if (has_exchange_ && concurrent_ && !opt_.naive) {
-      // Concurrent pipeline (per chunk c), three streams:
-      //   B (bstream_): wait halo(c), interior(c-1) -> boundary units(c) -> evB[c&1]
-      //   C (comm_)   : wait evB[c&1] -> halo exchange of chunk c+1 (from boundary outputs)
-      //   I (compute_): wait evB[(c-1)&1] -> interior units(c) -> evI[c&1]
-      // The exchange latency is off the critical path as long as boundary + exchange
-      // fit under the interior launch.
-      bool check = false;
-      int k = next_chunk(steps_done_, target, &check);
-      H2D_HIP_CHECK(hipEventRecord(ev_i_[1], compute_));
-      H2D_HIP_CHECK(hipEventRecord(ev_b_[1], compute_));
-      if (k > 0) {
-        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_i_[1], 0));
-        trace_begin("exchange", comm_);
-        do_exchange_async(k);
-        trace_end("exchange", comm_);
-        H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
-        ++st.exchanges;
-      }
-      int c = 0;
-      while (k > 0) {
-        const int p = c & 1, q = p ^ 1;
-        H2D_HIP_CHECK(hipStreamWaitEvent(bstream_, ev_halo_, 0));
-        H2D_HIP_CHECK(hipStreamWaitEvent(bstream_, ev_i_[q], 0));
-        const int src = tiles_[0].cur;
-        trace_begin("boundary", bstream_);
-        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2, src, bstream_);
-        trace_end("boundary", bstream_);
-        H2D_HIP_CHECK(hipEventRecord(ev_b_[p], bstream_));
-        for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
-        bool check_next = false;
-        const int k_next = next_chunk(steps_done_ + k, target, &check_next);
-        if (k_next > 0) {
-          H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_b_[p], 0));
-          trace_begin("exchange", comm_);
-          do_exchange_async(k_next);
-          trace_end("exchange", comm_);
-          H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
-          ++st.exchanges;
-        }
-        H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[q], 0));
-        trace_begin("interior", compute_);
-        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1, src, compute_);
-        trace_end("interior", compute_);
-        H2D_HIP_CHECK(hipEventRecord(ev_i_[p], compute_));
-        ++st.chunks;
-        if (check) {
-          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_b_[p], 0));
-          for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
-          if (fused_) {
-            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
-          } else {
-            st.residual = finish_residual();
-            if (st.residual < opt_.sensitivity) {
-              rollback();
-              st.converged = true;
-              break;
-            }
-          }
-        }
-        steps_done_ += k;
-        k = k_next;
-        check = check_next;
-        ++c;
-      }
-      H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
-      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
-      H2D_HIP_CHECK(hipEventRecord(ev_ready_, bstream_));
-      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
-    } else if (has_exchange_ && opt_.overlap && !opt_.naive) {
-      // Boundary-first pipeline (per chunk c):
-      //   compute: wait halo(c) -> boundary units(c) -> [event] -> interior units(c)
-      //   comm   : wait boundary(c) -> exchange the halo of chunk c+1 from the boundary outputs
-      // Boundary units are short (they gate the exchange); the exchange of chunk c+1 runs
-      // under the interior units of chunk c.
-      bool check = false;
-      int k = next_chunk(steps_done_, target, &check);
-      if (k > 0) {
-        H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
-        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
-        trace_begin("exchange", comm_);
-        do_exchange_async(k);
-        trace_end("exchange", comm_);
-        H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
-        ++st.exchanges;
-      }
-      while (k > 0) {
-        H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
-        trace_begin("boundary", compute_);
-        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 2);
-        trace_end("boundary", compute_);
-        H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
-        const int src = tiles_[0].cur;
-        for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
-        bool check_next = false;
-        const int k_next = next_chunk(steps_done_ + k, target, &check_next);
-        if (k_next > 0) {
-          H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
-          trace_begin("exchange", comm_);
-          do_exchange_async(k_next);
-          trace_end("exchange", comm_);
-          H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
-          ++st.exchanges;
-        }
-        trace_begin("interior", compute_);
-        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 1, src);
-        trace_end("interior", compute_);
-        ++st.chunks;
-        if (check) {
-          for (int t = 0; t < (int)tiles_.size(); ++t) reduce_tile_residual(t, k);
-          if (fused_) {
-            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
-          } else {
-            st.residual = finish_residual();
-            if (st.residual < opt_.sensitivity) {
-              rollback();
-              st.converged = true;
-              break;
-            }
-          }
-        }
-        steps_done_ += k;
-        k = k_next;
-        check = check_next;
-      }
-      // join the comm stream (a speculative exchange may still be in flight)
-      H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
-      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
     } else {
       while (steps_done_ < target) {
         bool check = false;
@@ -1510,7 +1340,7 @@ void Engine::device_decide(unsigned long long seq) {
     ++ipc_resid_epoch_;
     launch_ipc_allreduce(d_resid_, total, d_ipc_blocks_, tiles_[0].rank, (int)ipc_blocks_.size(),
                          (int)(ipc_resid_epoch_ & 1), (unsigned long long)ipc_blocks_.size() * ipc_resid_epoch_,
-                         ipc_lay_.resid_count, ipc_lay_.resid_slots, kIpcMaxRanks,
+                         ipc_lays_[tiles_[0].rank].resid_count, ipc_lays_[tiles_[0].rank].resid_slots, kIpcMaxRanks,
                          std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6)), d_sig_timeout_,
                          h_timeout_dev_, d_stop_, &d, compute_);
   } else if (rccl_comm_) {
@@ -1776,14 +1606,16 @@ void Engine::init_rccl(const std::string& id, int nranks, int rank) {
 
 // ---- IPC direct transport ----------------------------------------------------------------
 
-void Engine::ipc_layout() {
+Engine::IpcLayout Engine::ipc_layout_of(int rank) const {
   // One uncached (MTYPE UC) device block per rank: every access goes to memory, so stores a
   // peer GPU makes over xGMI are seen by plain loads here without any cache maintenance, and
   // polls of the flags see the peers' atomics.  Flags and counters on lines of their own.
-  const TileGeom& g = tiles_.at(0).g;
+  // Computed from the decomposition alone, so every rank knows every rank's layout.
+  const TileGeom g = dec_.tile(rank, G_);
   const size_t rb = (size_t)g.G * (size_t)g.pitch * sizeof(float);  // G full storage rows
   const size_t rs = (rb + 4095) & ~size_t(4095);
   IpcLayout L;
+  for (int d = 0; d < kNumDirs; ++d) L.flag[d] = 128 * (size_t)d;
   size_t off = 4096;  // flags / residual slots live in the first 4 KiB
   for (int p = 0; p < 2; ++p) {
     L.recv_n[p] = off;
@@ -1793,23 +1625,60 @@ void Engine::ipc_layout() {
     L.recv_s[p] = off;
     off += rs;
   }
+  L.pitch = g.pitch;
+  bool side = false;
+  for (int d = kW; d < kNumDirs; ++d) side = side || dec_.neighbor(rank, d) >= 0;
+  if (side) {
+    // W / E ghost-column groups (kGhostGroup columns per side and parity) in rows [-G, xcell+G),
+    // with the tile's pitch (the streaming kernel's ghost lanes read them like tile rows)
+    L.xbuf = off;
+    off += (((size_t)(g.xcell + 2 * g.G) * (size_t)g.pitch * sizeof(float)) + 4095) & ~size_t(4095);
+  }
   L.bytes = off;
-  static_assert(512 + 2 * kIpcMaxRanks * sizeof(double) <= 4096, "IPC residual slots overflow the header");
-  ipc_lay_ = L;
+  static_assert(1152 + 2 * kIpcMaxRanks * sizeof(double) <= 4096, "IPC residual slots overflow the header");
+  return L;
+}
+
+float* Engine::side_push_base(int d, int pr, int q) const {
+  // My cell (i, j) that lies in neighbour pr's halo (direction d) is stored at
+  // base + i * pitch(pr) + j: every offset of its ghost-column group folded in.
+  const TileGeom& g = tiles_.at(0).g;
+  const TileGeom n = dec_.tile(pr, G_);
+  const IpcLayout& L = ipc_lays_[pr];
+  const int64_t P = L.pitch;
+  const bool west_of_me = d == kW || d == kNW || d == kSW;  // my first columns -> its E group
+  int64_t row0 = g.G;                                       // my row i -> its row i (W, E)
+  if (d == kNW || d == kNE) row0 = g.G + n.xcell;           // my row i < G -> its row xcell_n + i
+  if (d == kSW || d == kSE) row0 = g.G - g.xcell;           // my row i >= xcell - G -> its row i - xcell
+  const int64_t col0 = west_of_me ? 0 : kGhostGroup - g.ycell;  // my column j -> its group column
+  const int64_t off = (int64_t)L.group(west_of_me ? 1 : 0, q) + (row0 * P + col0) * (int64_t)sizeof(float);
+  return reinterpret_cast<float*>(ipc_blocks_[pr] + off);
 }
 
 std::string Engine::ipc_handle() {
   if (transport_ != kTransportIpc) throw std::logic_error("ipc_handle: engine transport is not IPC");
   if (!ipc_block_) {
-    ipc_layout();
+    ipc_lays_.assign(dec_.nranks(), IpcLayout());
+    for (int r = 0; r < dec_.nranks(); ++r) ipc_lays_[r] = ipc_layout_of(r);
     H2D_HIP_CHECK(hipSetDevice(opt_.device));
-    H2D_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&ipc_block_), ipc_lay_.bytes, hipDeviceMallocUncached));
-    H2D_HIP_CHECK(hipMemset(ipc_block_, 0, ipc_lay_.bytes));
+    const IpcLayout& L = ipc_lays_[tiles_.at(0).rank];
+    H2D_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&ipc_block_), L.bytes, hipDeviceMallocUncached));
+    H2D_HIP_CHECK(hipMemset(ipc_block_, 0, L.bytes));
     H2D_HIP_CHECK(hipDeviceSynchronize());
   }
   hipIpcMemHandle_t h;
   H2D_HIP_CHECK(hipIpcGetMemHandle(&h, ipc_block_));
-  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+  // the handle, then this rank's push counts per (K, direction): what its neighbours' halo
+  // waits count per chunk
+  std::vector<int32_t> counts((size_t)(G_ + 1) * kNumDirs, 0);
+  for (int K = 1; K <= G_; ++K)
+    if (stream_k_supported(K)) {
+      const UnitLists& U = units(0, K);
+      for (int d = 0; d < kNumDirs; ++d) counts[(size_t)K * kNumDirs + d] = U.pushes[d];
+    }
+  std::string blob(reinterpret_cast<const char*>(&h), sizeof(h));
+  blob.append(reinterpret_cast<const char*>(counts.data()), counts.size() * sizeof(int32_t));
+  return blob;
 }
 
 void Engine::ipc_open(const std::vector<std::string>& handles) {
@@ -1817,15 +1686,20 @@ void Engine::ipc_open(const std::vector<std::string>& handles) {
   const int me = tiles_.at(0).rank, nr = dec_.nranks();
   if ((int)handles.size() != nr) throw std::invalid_argument("ipc_open: one handle per rank expected");
   if (nr > kIpcMaxRanks) throw std::invalid_argument("ipc_open: too many ranks");
+  const size_t want = sizeof(hipIpcMemHandle_t) + (size_t)(G_ + 1) * kNumDirs * sizeof(int32_t);
   H2D_HIP_CHECK(hipSetDevice(opt_.device));
   ipc_blocks_.assign(nr, nullptr);
   ipc_opened_.assign(nr, false);
+  ipc_counts_.assign(nr, std::vector<int32_t>());
   for (int r = 0; r < nr; ++r) {
+    if (handles[r].size() != want) throw std::invalid_argument("ipc_open: bad handle (another build or halo depth?)");
+    ipc_counts_[r].resize((size_t)(G_ + 1) * kNumDirs);
+    std::memcpy(ipc_counts_[r].data(), handles[r].data() + sizeof(hipIpcMemHandle_t),
+                ipc_counts_[r].size() * sizeof(int32_t));
     if (r == me) {
       ipc_blocks_[r] = ipc_block_;
       continue;
     }
-    if (handles[r].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("ipc_open: bad handle");
     hipIpcMemHandle_t h;
     std::memcpy(&h, handles[r].data(), sizeof(h));
     void* p = nullptr;
@@ -1835,7 +1709,7 @@ void Engine::ipc_open(const std::vector<std::string>& handles) {
     // the mapping must work before any kernel dereferences it (a fault here is an error, not a
     // GPU memory fault inside the stencil)
     unsigned long long probe = 0;
-    H2D_HIP_CHECK(hipMemcpy(&probe, ipc_blocks_[r] + ipc_lay_.flag_n, sizeof(probe), hipMemcpyDeviceToHost));
+    H2D_HIP_CHECK(hipMemcpy(&probe, ipc_blocks_[r], sizeof(probe), hipMemcpyDeviceToHost));
   }
   d_ipc_blocks_ = dmalloc<char*>((size_t)nr);
   H2D_HIP_CHECK(hipMemcpy(d_ipc_blocks_, ipc_blocks_.data(), nr * sizeof(char*), hipMemcpyHostToDevice));
@@ -1844,8 +1718,8 @@ void Engine::ipc_open(const std::vector<std::string>& handles) {
 
 void Engine::ipc_prime() {
   // Collective (the caller brackets it with barriers: no kernel of any rank is running):
-  // zero my flags and counters, and write my boundary rows into the neighbours' receive
-  // buffers of parity 0 (what their chunk 0 reads) — the initial halo.
+  // zero my flags and counters, and write my boundary rows / columns / corners into the
+  // neighbours' receive buffers of parity 0 (what their chunk 0 reads) — the initial halo.
   if (ipc_blocks_.empty()) throw std::logic_error("ipc_prime: call ipc_open() first");
   H2D_HIP_CHECK(hipSetDevice(opt_.device));
   H2D_HIP_CHECK(hipDeviceSynchronize());
@@ -1857,13 +1731,26 @@ void Engine::ipc_prime() {
   const char* cur = reinterpret_cast<const char*>(T.buf[T.cur]);
   const size_t row = (size_t)g.pitch * sizeof(float);
   if (pn >= 0)  // my rows [0, G) -> N's receive buffer for its south ghost rows
-    H2D_HIP_CHECK(hipMemcpy(ipc_blocks_[pn] + ipc_lay_.recv_s[0], cur + (size_t)g.G * row, rb, hipMemcpyDeviceToDevice));
-  if (ps >= 0)  // my rows [xcell - G, xcell) -> S's receive buffer for its north ghost rows
-    H2D_HIP_CHECK(hipMemcpy(ipc_blocks_[ps] + ipc_lay_.recv_n[0], cur + (size_t)g.xcell * row, rb,
+    H2D_HIP_CHECK(hipMemcpy(ipc_blocks_[pn] + ipc_lays_[pn].recv_s[0], cur + (size_t)g.G * row, rb,
                             hipMemcpyDeviceToDevice));
+  if (ps >= 0)  // my rows [xcell - G, xcell) -> S's receive buffer for its north ghost rows
+    H2D_HIP_CHECK(hipMemcpy(ipc_blocks_[ps] + ipc_lays_[ps].recv_n[0], cur + (size_t)g.xcell * row, rb,
+                            hipMemcpyDeviceToDevice));
+  for (int d = kW; d < kNumDirs; ++d) {
+    const int pr = dec_.neighbor(T.rank, d);
+    if (pr < 0) continue;
+    // my cells of its halo: columns [0, G) or [ycell - G, ycell); rows all, [0, G) or [xcell - G, xcell)
+    const bool west = d == kW || d == kNW || d == kSW;
+    const int64_t c0 = west ? 0 : g.ycell - g.G;
+    const int64_t r0 = (d == kSW || d == kSE) ? g.xcell - g.G : 0;
+    const int64_t nrows = (d == kW || d == kE) ? g.xcell : g.G;
+    float* dst = side_push_base(d, pr, 0) + r0 * ipc_lays_[pr].pitch + c0;
+    H2D_HIP_CHECK(hipMemcpy2D(dst, (size_t)ipc_lays_[pr].pitch * sizeof(float), T.buf[T.cur] + g.idx(r0, c0), row,
+                              (size_t)g.G * sizeof(float), (size_t)nrows, hipMemcpyDeviceToDevice));
+  }
   H2D_HIP_CHECK(hipDeviceSynchronize());
   ipc_chunk_ = 0;
-  ipc_need_[0] = ipc_need_[1] = 0;
+  for (auto& v : ipc_need_) v = 0;
   ipc_resid_epoch_ = 0;
   ipc_primed_ = true;
 }
@@ -1877,8 +1764,8 @@ double Engine::ipc_allreduce_residual() {
   ++ipc_resid_epoch_;
   const int nr = (int)ipc_blocks_.size();
   launch_ipc_allreduce(d_resid_, d_resid_ + tiles_.size(), d_ipc_blocks_, tiles_[0].rank, nr,
-                       (int)(ipc_resid_epoch_ & 1), (unsigned long long)nr * ipc_resid_epoch_, ipc_lay_.resid_count,
-                       ipc_lay_.resid_slots, kIpcMaxRanks,
+                       (int)(ipc_resid_epoch_ & 1), (unsigned long long)nr * ipc_resid_epoch_,
+                       ipc_lays_[tiles_[0].rank].resid_count, ipc_lays_[tiles_[0].rank].resid_slots, kIpcMaxRanks,
                        std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6)), d_sig_timeout_,
                        h_timeout_dev_, nullptr, nullptr, compute_);
   H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_ + tiles_.size(), sizeof(double), hipMemcpyDeviceToHost, compute_));

@@ -56,10 +56,6 @@ struct EngineOptions {
   double row_edge_weight = -1.0;  // ... of a row-edge unit (<= 0: edge_weight)
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   int boundary_rows = 8;      // rows per halo-dependent work unit (overlap mode; at least K)
-  int concurrent = -1;        // boundary units on a second stream: -1 auto, 0 never, 1 always
-  // concurrent pipeline shape: boundary units on the comm stream ahead of the exchange they
-  // feed (two streams; default), or on a third stream of their own (0)
-  int comm_boundary = -1;
   // Signalled pipeline: ONE launch per chunk with the halo-dependent units first; each of them
   // bumps a counter when its rows are final and the comm stream starts the exchange of the
   // next chunk as soon as the counter says so (mid-kernel).  -1 auto, 0 off,
@@ -121,11 +117,11 @@ struct EngineOptions {
   int comm_cus = -1;
   int comm_cu_layout = 0;
   // Resident-wave slots the interior launch leaves free for kernels that run beside it (the
-  // RCCL p2p kernel and, in the concurrent pipeline, the boundary units).  The dispatcher
+  // RCCL p2p kernel of the signalled pipeline).  The dispatcher
   // deals waves round-robin over XCDs and shader engines, so a kernel launched second only
   // finds a slot if every engine keeps some free.  -1 auto.
   int reserve_waves = -1;
-  bool device_fence_events = false;  // pipeline events without the system-scope fence  // reserved CU indices: 0 spread evenly, 1 the highest, 2 the lowest
+  bool device_fence_events = false;  // pipeline events without the system-scope fence
   // RCCL: send/receive whole K-row halos straight from/into the tile (no pack/unpack) when
   // the decomposition has no west/east neighbours (1-D row strips).  -1 auto, 0 off.
   int contiguous_halo = -1;
@@ -159,13 +155,12 @@ class Engine {
   int halo_depth() const { return G_; }
   bool on_gpu() const { return opt_.device >= 0; }
   bool has_exchange() const { return has_exchange_; }
-  bool concurrent() const { return concurrent_; }
   int signal_mode() const { return sig_mode_; }
   bool tiled() const { return tiled_; }
   std::vector<int> tile_config() const { return {tile_tx_, tile_ry_, tile_k_}; }
   int tile_threads() const { return tile_nt_; }
   int tile_cpl() const { return tile_cpl_; }
-  // "none" (no exchange), "signal", "concurrent", "concurrent3", "boundary-first", "serial"
+  // "none" (no exchange), "direct" (IPC), "external", "signal", "serial"
   std::string pipeline() const;
   int rows_per_wave(int K) const;  // largest unit height for depth K (tile 0)
   int num_units(int K) const;      // work units (waves) per chunk of depth K, all tiles
@@ -250,6 +245,7 @@ class Engine {
     int sig_rows = 0;          // > 0: boundary units are full-size and signal after this many rows
     int n_all = 0, n_interior = 0, n_boundary = 0;
     int n_dir[2] = {0, 0};     // halo units facing north (top) / south (bottom, kUnitReverse)
+    int pushes[kNumDirs] = {};  // units pushing to the neighbour in each direction (direct pipeline)
   };
 
   const UnitLists& units(int t, int K);
@@ -290,9 +286,7 @@ class Engine {
   int64_t steps_done_ = 0;
 
   // device state
-  hipStream_t compute_ = nullptr, comm_ = nullptr, bstream_ = nullptr;
-  hipEvent_t ev_i_[2] = {nullptr, nullptr}, ev_b_[2] = {nullptr, nullptr};
-  bool concurrent_ = false;
+  hipStream_t compute_ = nullptr, comm_ = nullptr;
   hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_t0_ = nullptr, ev_t1_ = nullptr, ev_done_ = nullptr;
   void end_of_run_wait(RunStats& st, std::chrono::steady_clock::time_point w0);
   std::map<std::pair<int, int>, UnitLists> units_;
@@ -331,20 +325,28 @@ class Engine {
   // ---- IPC direct transport ----
   bool direct_ = false;
   struct IpcLayout {
-    size_t flag_n = 0, flag_s = 128, resid_count = 256, resid_slots = 512;  // byte offsets
+    size_t flag[kNumDirs] = {};                   // pushes arrived from the neighbour in direction d
+    size_t resid_count = 1024, resid_slots = 1152;  // byte offsets
     size_t recv_n[2] = {0, 0}, recv_s[2] = {0, 0};
+    size_t xbuf = 0;     // W / E ghost-column groups (2-D blocks only; 0: none)
+    int64_t pitch = 0;   // the tile's row pitch (floats): also the xbuf's
     size_t bytes = 0;
-  } ipc_lay_;
+    // group (side 0 W / 1 E, parity p): its column 0 in xbuf row 0 (= tile row -G)
+    size_t group(int side, int p) const { return xbuf + (size_t)(2 * side + p) * kGhostGroup * sizeof(float); }
+  };
   static constexpr int kIpcMaxRanks = 64;
+  IpcLayout ipc_layout_of(int rank) const;
+  float* side_push_base(int d, int peer_rank, int parity) const;
+  std::vector<IpcLayout> ipc_lays_;         // every rank's block layout (from the decomposition)
+  std::vector<std::vector<int32_t>> ipc_counts_;  // per rank: units pushing per (K, direction)
   char* ipc_block_ = nullptr;               // my uncached block: flags, residual slots, receive buffers
   std::vector<char*> ipc_blocks_;           // every rank's block (mine included), mapped
   std::vector<bool> ipc_opened_;            // entries from hipIpcOpenMemHandle (closed in the dtor)
   char** d_ipc_blocks_ = nullptr;           // device copy of ipc_blocks_
   bool ipc_primed_ = false;
   unsigned long long ipc_chunk_ = 0;        // chunks since the prime (receive-buffer parity)
-  unsigned long long ipc_need_[2] = {0, 0};  // halo pushes expected from north / south
+  unsigned long long ipc_need_[kNumDirs] = {};  // halo pushes expected from each direction (cumulative)
   unsigned long long ipc_resid_epoch_ = 0;  // residual all-reduces since the prime
-  void ipc_layout();
   // ---- device-side convergence ----
   bool fused_ = false;
   unsigned long long* d_stop_ = nullptr;  // 0 running, else the sequence number of the converged check

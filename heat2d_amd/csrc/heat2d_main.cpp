@@ -320,15 +320,16 @@ int main(int argc, char** argv) {
   if (dev == "gpu" && ndev == 0) usage("--device gpu but no HIP device is visible");
   o.device = dev == "gpu" ? env.local_rank % std::max(1, ndev) : -1;
   o.transport = kTransportLocal;
-  // multi-rank: one tile per process; GPUs: the direct IPC halo pipeline for 1-D row strips,
-  // RCCL otherwise; CPUs: halos relayed through the bootstrap
-  const bool rows = o.gridy == 1 && !o.periodic_y;
+  // multi-rank: one tile per process; GPUs: the direct IPC halo pipeline (rows or blocks),
+  // RCCL where it cannot run; CPUs: halos relayed through the bootstrap
   const std::string tsel = a.count("transport") ? a["transport"] : "auto";
   if (world > 1) {
     o.ranks = {env.rank};
     if (dev != "gpu") o.transport = kTransportExternal;
-    // direct IPC needs halo units of at least max(K, G) rows at both ends of every strip
-    else if (tsel == "ipc" || (tsel == "auto" && rows && o.nx / o.gridx >= 2 * (int64_t)o.tblock))
+    // direct IPC needs halo units of at least max(K, G) rows at both ends of every strip (and,
+    // for 2-D blocks, tiles 4-column aligned: the engine refuses others and every rank falls
+    // back to RCCL together below)
+    else if (tsel == "ipc" || (tsel == "auto" && o.nx / o.gridx >= 2 * (int64_t)o.tblock))
       o.transport = kTransportIpc;
     else o.transport = kTransportRccl;
   }

@@ -32,14 +32,24 @@ namespace h2d {
 // [olo, ohi): the strip's output columns.  Interior strips have cb = olo - R; a strip against
 // a FIXED global edge column is aligned to that edge and needs no outer cone (the held edge
 // column is valid at every level), so it outputs 256 - R columns (strip_layout).
+// links (2-D direct pipeline): bits 0-5 — the unit's K-cone reads the ghost side W, E, NW, NE,
+// SW, SE (kLink*), so it waits for that neighbour's pushes; bits 8-13 — its outputs are part of
+// that neighbour's halo, so it pushes them there and signals at its end.  kUnitNS: the unit is
+// the top (north) or, with kUnitReverse, bottom (south) halo unit of its strip.
 struct Unit {
   int strip;
   int x0;
   int h;
   int flags;
   int cb, olo, ohi;
+  int links;
 };
-constexpr int kEdgeCols = 1, kEdgeRows = 2, kUnitReverse = 4, kUnitSigEnd = 8;
+constexpr int kEdgeCols = 1, kEdgeRows = 2, kUnitReverse = 4, kUnitSigEnd = 8, kUnitNS = 16;
+// side links, indexed like Dir - 2 (kW .. kSE)
+constexpr int kLinkW = 1, kLinkE = 2, kLinkNW = 4, kLinkNE = 8, kLinkSW = 16, kLinkSE = 32;
+constexpr int kSideLinks = 6;
+// columns of one ghost-column group of the 2-D direct receive buffer (>= the deepest lead R)
+constexpr int kGhostGroup = 16;
 
 int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t cb, bool fixed, bool per_x, bool per_y);
 // Column strips of a tile for depth K.  Interior strips output 256 - 2R columns; with fixed
@@ -119,6 +129,20 @@ struct StreamArgs {
   // then carry on (kUnitSigEnd: at the unit's end).
   int nsignal = 0;
   int sig_rows = 0;
+  // 2-D direct pipeline, side links (index = Dir - 2: W, E, NW, NE, SW, SE):
+  //   xwait[i]/xneed[i]: my flag for pushes from that neighbour and the count this chunk needs;
+  //   xsig[i]:           that neighbour's flag for my pushes;
+  //   gsrc[0/1]:         my W / E ghost-column group of this chunk's parity — ghost column j of
+  //                      row i lives at gsrc[0] + (G + i) * pitch + kGhostGroup + j (j < 0) and
+  //                      gsrc[1] + (G + i) * pitch + (j - ycell) (j >= ycell);
+  //   xpush[i]/xpitch[i]: my cell (i, j) that belongs to that neighbour's halo is stored at
+  //                      xpush[i] + i * xpitch[i] + j (the host folds every offset into xpush).
+  const unsigned long long* xwait[kSideLinks] = {};
+  unsigned long long xneed[kSideLinks] = {};
+  unsigned long long* xsig[kSideLinks] = {};
+  const float* gsrc[2] = {nullptr, nullptr};
+  float* xpush[kSideLinks] = {};
+  int64_t xpitch[kSideLinks] = {};
   unsigned long long* sig[2] = {nullptr, nullptr};
   const unsigned long long* wait[2] = {nullptr, nullptr};
   unsigned long long need[2] = {0, 0};

@@ -126,7 +126,33 @@ struct LaneCtx {
   float* obase;
   int obo, obs;
   unsigned voff;
+  // 2-D direct pipeline side pushes (Unit::links bits 8-13), per output row orow at tile row
+  // xr0 + xdir * orow: sp (W or E neighbour: every row), cn (NW / NE: rows < G), cs (SW / SE:
+  // rows >= xcell - G), each with its per-orow step; em: the lane's elements that are pushed.
+  bool spu;  // wave-uniform: the unit pushes to a side or corner
+  unsigned em;
+  float *sp, *cn, *cs;
+  int64_t sps, cns, css;
+  int64_t xr0, xdir, xlo, xhi;
 };
+
+// Masked element stores (a lane's float4 can straddle the G-column boundary of a side push).
+__device__ __forceinline__ void store_masked(float* p, const float4& o, unsigned m) {
+  if (m & 1u) p[0] = o.x;
+  if (m & 2u) p[1] = o.y;
+  if (m & 4u) p[2] = o.z;
+  if (m & 8u) p[3] = o.w;
+}
+
+// 2-D direct pipeline: this output row's cells that lie in a W/E neighbour's halo (and, in the
+// first / last G rows, a corner neighbour's) go straight into that neighbour's receive columns.
+__device__ __forceinline__ void side_push(const float4& o, int64_t orow, const LaneCtx& c) {
+  if (c.em == 0u) return;
+  const int64_t r = c.xr0 + c.xdir * orow;
+  if (c.sp != nullptr) store_masked(c.sp + orow * c.sps, o, c.em);
+  if (c.cn != nullptr && r < c.xlo) store_masked(c.cn + orow * c.cns, o, c.em);
+  if (c.cs != nullptr && r >= c.xhi) store_masked(c.cs + orow * c.css, o, c.em);
+}
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -185,7 +211,7 @@ __device__ __forceinline__ float4 apply_edge(float4 o, const float4& C, int64_t 
 // Process stream input row `ir` (level-0 value `cur`) through levels 1..TMAX (TMAX <= K).
 // Slot parity P = ir & 1: S[l][P] holds level-l row (ir-l-2), S[l][1-P] holds row (ir-l-1).
 // Level t computes row (ir - t) of level t.  Level K writes output row ir - 2K (unit-relative).
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, int P, int TMAX>
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int P, int TMAX>
 __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int ir, const LaneCtx& c, const Coef& k,
                                             double& racc) {
 #pragma unroll
@@ -204,6 +230,7 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
       if constexpr (WT) store_row_wt(c.obase, c.voff, c.obo + (int)orow * c.obs, o);
       else *reinterpret_cast<float4*>(c.sout + orow * c.spitch) = o;
       if (orow < c.prows) *reinterpret_cast<float4*>(c.pout + orow * c.ppitch) = o;  // uniform branch
+      if constexpr (SIDE) side_push(o, orow, c);
       if constexpr (RESID) {
         *reinterpret_cast<float4*>(c.kout + orow * c.kpitch) = mid;
         racc += c.st0 ? sq_diff(o.x, mid.x) : 0.0;
@@ -216,17 +243,13 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
   }
 }
 
-// Prologue row IR (compile-time): levels t <= IR/2 are primed.
-// Stream rows [0, K) are the unit's outer cone rows: for a halo unit, the ghost rows, read from
-// hrowp (the halo receive buffer of the direct pipeline; == rowp otherwise).
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, int IR>
-__device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4* __restrict__ rowp,
-                                         const float4* __restrict__ hrowp, int64_t pitch4, const LaneCtx& c,
+// Prologue row IR (compile-time): levels t <= IR/2 are primed, from rows already in registers.
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int IR>
+__device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4 (&pro)[2 * K], const LaneCtx& c,
                                          const Coef& k, double& racc) {
   if constexpr (IR < 2 * K) {
-    const float4 v = (IR < K ? hrowp : rowp)[(int64_t)IR * pitch4];
-    process_row<K, F32, EDGE, FIXED, RESID, WT, IR & 1, IR / 2>(S, v, IR, c, k, racc);
-    prologue<K, F32, EDGE, FIXED, RESID, WT, IR + 1>(S, rowp, hrowp, pitch4, c, k, racc);
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR & 1, IR / 2>(S, pro[IR], IR, c, k, racc);
+    prologue<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR + 1>(S, pro, c, k, racc);
   }
 }
 
@@ -248,7 +271,7 @@ __device__ __forceinline__ void unit_signal(unsigned long long* sig, int lane, i
 
 // sig_at > 0: signal (once) before processing stream row sig_at (a multiple of 4 past 2K),
 // i.e. once every output row < sig_at - 2K is stored.
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT>
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE>
 __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const float4* __restrict__ hrowp,
                                          int64_t pitch4, int n, const LaneCtx& c, const Coef& k, double& racc,
                                          int sig_at, unsigned long long* sig, int lane) {
@@ -258,18 +281,27 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
     S[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
     S[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // n = h + 2K >= 2K + 1: the prologue rows all exist.  Prefetch the first steady rows first.
+  // n = h + 2K >= 2K + 1: the prologue rows all exist.  Every prologue row and the first four
+  // steady rows are loaded up front, all in flight at once: ONE memory round trip starts the
+  // unit (left to the scheduler, each prologue load sat behind the previous row's compute and a
+  // vmcnt(0) — several serialised round trips, ~3 us of every launch).  Stream rows [0, K) are
+  // the unit's outer cone rows: for a halo unit, the ghost rows, read from hrowp (the halo
+  // receive buffer of the direct pipeline; == rowp otherwise).
+  float4 pro[2 * K];
+#pragma unroll
+  for (int i = 0; i < 2 * K; ++i) pro[i] = (i < K ? hrowp : rowp)[(int64_t)i * pitch4];
   float4 pf[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(2 * K + d, n - 1) * pitch4];
-  prologue<K, F32, EDGE, FIXED, RESID, WT, 0>(S, rowp, hrowp, pitch4, c, k, racc);
+  __builtin_amdgcn_sched_barrier(0);  // keep the loads above: each use waits only for its own row
+  prologue<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0>(S, pro, c, k, racc);
 
   int ir0 = 2 * K;  // even: slot parity of sub-step d is d & 1
 #define H2D_STEADY(D)                                                        \
   {                                                                          \
     const float4 nw = pf[D];                                                 \
     pf[D] = rowp[(int64_t)min(ir0 + (D) + 4, n - 1) * pitch4];               \
-    process_row<K, F32, EDGE, FIXED, RESID, WT, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
   for (; ir0 + 4 <= n; ir0 += 4) {
     if (ir0 == sig_at) unit_signal(sig, lane, c.rel);
@@ -280,9 +312,9 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
   }
 #undef H2D_STEADY
   // tail: at most 3 rows
-  if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, 0, K>(S, pf[0], ir0, c, k, racc);
-  if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
-  if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
+  if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0, K>(S, pf[0], ir0, c, k, racc);
+  if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
+  if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
   // the loop visits every sig_at candidate below its exit value: a signal point at or past the
   // exit has not fired yet (unit shorter than its signal rows, or kUnitSigEnd)
   if (sig_at >= ir0) unit_signal(sig, lane, c.rel);
@@ -302,12 +334,12 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-template <int K, bool F32, bool RESID, bool WT, int EDGE>
+template <int K, bool F32, bool RESID, bool WT, int EDGE, bool SIDE = false>
 __device__ __forceinline__ void run_edge(const float4* rowp, const float4* hrowp, int64_t pitch4, int n,
                                          const LaneCtx& c, const Coef& k, double& racc, bool fixed, int sig_at,
                                          unsigned long long* sig, int lane) {
-  if (fixed) run_unit<K, F32, EDGE, true, RESID, WT>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
-  else run_unit<K, F32, EDGE, false, RESID, WT>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+  if (fixed) run_unit<K, F32, EDGE, true, RESID, WT, SIDE>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+  else run_unit<K, F32, EDGE, false, RESID, WT, SIDE>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
 }
 
 // The decision of a convergence check, by the one lane that holds the total.
@@ -357,27 +389,45 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const unsigned long long t_start = stamping ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const Unit u = a.units[w];
   const bool halo_unit = w < a.nsignal;
+  const bool ns_unit = halo_unit && (u.flags & kUnitNS) != 0;  // top / bottom halo unit of its strip
   const int dir = (u.flags & kUnitReverse) ? 1 : 0;  // 0: north halo (top unit), 1: south (bottom unit)
+  const int xreads = halo_unit ? (u.links & 0x3f) : 0;          // 2-D direct: side ghosts read
+  const int xpushes = halo_unit ? ((u.links >> 8) & 0x3f) : 0;  // 2-D direct: sides pushed to
   if (a.stop != nullptr && __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) {
     // converged earlier in this run: no work, but halo units still count, so gates / flags of
     // launches already queued on other streams and ranks stay in step
-    if (halo_unit && a.sig[dir] != nullptr && lane == 0)
+    if (ns_unit && a.sig[dir] != nullptr && lane == 0)
       __hip_atomic_fetch_add(a.sig[dir], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0)
+      for (int i = 0; i < kSideLinks; ++i)
+        if ((xpushes >> i) & 1) __hip_atomic_fetch_add(a.xsig[i], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
-  if (halo_unit && a.wait[dir] != nullptr) {
+  const bool ns_wait = ns_unit && a.wait[dir] != nullptr;
+  if (ns_wait || xreads != 0) {
     // wait until the exchange that fills this unit's ghost rows has landed (a wait that already
     // timed out in this engine stops every later wait: fail fast)
     if (lane == 0 && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       long long i = 0;
       // relaxed polls (an acquire per poll is 2-3x slower per hop), ONE acquire after the match
-      while (__hip_atomic_load(a.wait[dir], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.need[dir]) {
-        if (++i > a.halo_polls) {
-          report_timeout(a.timed_out, a.timed_out_host, 2u);
-          break;
+      if (ns_wait)
+        while (__hip_atomic_load(a.wait[dir], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.need[dir]) {
+          if (++i > a.halo_polls) {
+            report_timeout(a.timed_out, a.timed_out_host, 2u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_s_sleep(2);
+      for (int x = 0; x < kSideLinks; ++x) {
+        if (((xreads >> x) & 1) == 0) continue;
+        while (__hip_atomic_load(a.xwait[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.xneed[x]) {
+          if (++i > a.halo_polls) {
+            report_timeout(a.timed_out, a.timed_out_host, 2u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
       }
       if (a.wait_acc != nullptr) {  // exposed halo wait of this unit (fire-and-forget atomics)
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
@@ -428,7 +478,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   c.st1 = in_out && cb + 1 < a.ycell;
   c.st2 = in_out && cb + 2 < a.ycell;
   c.st3 = in_out && cb + 3 < a.ycell;
-  const bool pushes = halo_unit && a.push[dir] != nullptr;
+  const bool pushes = ns_unit && a.push[dir] != nullptr;
   c.prows = pushes ? a.sig_rows : 0;
   c.rel = a.rel;
   const bool keeps = a.keep != nullptr && in_out;
@@ -437,24 +487,86 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   c.pout = (pushes && in_out) ? a.push[dir] + xout * a.pitch + a.PL + cb : a.dummy + 4 * lane;
   c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
 
+  // 2-D direct side pushes: this lane's elements in the W / E neighbour's halo columns
+  c.spu = xpushes != 0;
+  c.em = 0u;
+  c.sp = c.cn = c.cs = nullptr;
+  c.sps = c.cns = c.css = 0;
+  c.xr0 = xout;
+  c.xdir = rev ? -1 : 1;
+  c.xlo = a.G;
+  c.xhi = a.xcell - a.G;
+  if (c.spu && in_out) {
+    const bool wl = cb < a.G && (xpushes & (kLinkW | kLinkNW | kLinkSW)) != 0;
+    const bool el = cb + 3 >= a.ycell - a.G && (xpushes & (kLinkE | kLinkNE | kLinkSE)) != 0;
+    for (int e = 0; e < 4; ++e) {
+      const int64_t q = cb + e;
+      if ((wl && q < a.G) || (el && !wl && q >= a.ycell - a.G && q < a.ycell)) c.em |= 1u << e;
+    }
+    const int side = wl ? 0 : 1, cn = wl ? 2 : 3, cs = wl ? 4 : 5;  // link index W/E, NW/NE, SW/SE
+    const int64_t sgn = rev ? -1 : 1;
+    if (c.em != 0u) {
+      if ((xpushes >> side) & 1) {
+        c.sp = a.xpush[side] + xout * a.xpitch[side] + cb;
+        c.sps = sgn * a.xpitch[side];
+      }
+      if ((xpushes >> cn) & 1) {
+        c.cn = a.xpush[cn] + xout * a.xpitch[cn] + cb;
+        c.cns = sgn * a.xpitch[cn];
+      }
+      if ((xpushes >> cs) & 1) {
+        c.cs = a.xpush[cs] + xout * a.xpitch[cs] + cb;
+        c.css = sgn * a.xpitch[cs];
+      }
+    }
+  }
+
   const int64_t soff = (a.G + xin) * a.pitch + a.PL + cb;
   const float4* rowp = reinterpret_cast<const float4*>(a.src + soff);
-  const float4* hrowp = (halo_unit && a.hsrc[dir] != nullptr) ? reinterpret_cast<const float4*>(a.hsrc[dir] + soff)
-                                                              : rowp;
+  const float4* hrowp = (ns_unit && a.hsrc[dir] != nullptr) ? reinterpret_cast<const float4*>(a.hsrc[dir] + soff)
+                                                            : rowp;
+  // 2-D direct: lanes entirely left of column 0 / at or right of ycell are ghost columns — they
+  // read every row (corners included) from my receive groups (the same pitch as the tile)
+  if (xreads != 0) {
+    const int64_t rb = (a.G + xin) * a.pitch;
+    if (cb < 0 && (xreads & (kLinkW | kLinkNW | kLinkSW)) != 0) {
+      rowp = hrowp = reinterpret_cast<const float4*>(a.gsrc[0] + rb + kGhostGroup + cb);
+    } else if (cb >= a.ycell && (xreads & (kLinkE | kLinkNE | kLinkSE)) != 0) {
+      rowp = hrowp = reinterpret_cast<const float4*>(a.gsrc[1] + rb + min(cb - a.ycell, (int64_t)(kGhostGroup - 4)));
+    }
+  }
   const int64_t pitch4 = rev ? -(a.pitch >> 2) : (a.pitch >> 2);
   const int n = h + 2 * K;
   Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
   double racc = 0.0;
   // signalling units: mid-unit signal point (or the end); others never signal
-  unsigned long long* sig = halo_unit ? a.sig[dir] : nullptr;
+  unsigned long long* sig = ns_unit ? a.sig[dir] : nullptr;
   const int sig_at = sig == nullptr ? -1
                      : ((u.flags & kUnitSigEnd) != 0 || a.sig_rows <= 0) ? (1 << 30)
                                                                           : 2 * K + ((a.sig_rows + 3) & ~3);
-  switch (u.flags & 3) {
-    case 0: run_unit<K, F32, 0, false, RESID, WT>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane); break;
-    case 1: run_edge<K, F32, RESID, WT, 1>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
-    case 2: run_edge<K, F32, RESID, WT, 2>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
-    default: run_edge<K, F32, RESID, WT, 3>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+  if (c.spu) {
+    // side-pushing units of the 2-D direct pipeline: their own bodies, so the push code costs the
+    // common bodies no registers (the host never gives such a unit a column-edge window)
+    if ((u.flags & 3) == 0) run_unit<K, F32, 0, false, RESID, WT, true>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+    else run_edge<K, F32, RESID, WT, 2, true>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane);
+  } else {
+    switch (u.flags & 3) {
+      case 0: run_unit<K, F32, 0, false, RESID, WT, false>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane); break;
+      case 1: run_edge<K, F32, RESID, WT, 1>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+      case 2: run_edge<K, F32, RESID, WT, 2>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+      default: run_edge<K, F32, RESID, WT, 3>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+    }
+  }
+  if (xpushes != 0) {
+    // side and corner pushes are complete: drain, release as the N/S signal does, then one
+    // count per neighbour pushed to
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    else if (a.rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      for (int i = 0; i < kSideLinks; ++i)
+        if ((xpushes >> i) & 1) __hip_atomic_fetch_add(a.xsig[i], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if constexpr (RESID) {
     racc = wave_sum(racc);

@@ -109,19 +109,21 @@ PIPELINE_OPTIONS = {
 
 
 def candidates(transport: str, pipeline: str, world: int, on_gpu: bool, distinct_devices: bool,
-               layout: str, rows_per_rank: int = 1 << 30, depth: int = 8) -> List[Tuple[str, str]]:
+               layout: str, rows_per_rank: int = 1 << 30, depth: int = 8,
+               cols_per_rank: int = 1 << 30) -> List[Tuple[str, str]]:
     """(transport, pipeline) pairs to try, in order: the requested one first, then the safer
     fallbacks.  A run is only timed with a pair that passed the gate.  Between distinct devices
     (never exercised on one GPU): direct IPC with the measured fences, direct IPC with
     system-scope fences, RCCL (signalled, then serial), and host staging over gloo as the last
-    resort (no device-to-device path at all).  Direct IPC needs row strips of at least
-    2 * depth rows (halo units of at least `depth` rows at both ends of every column strip)."""
+    resort (no device-to-device path at all).  Direct IPC needs tiles of at least 2 * depth rows
+    (halo units of at least `depth` rows at both ends of every column strip) and, with west /
+    east neighbours (blocks), a width that is a multiple of 4 and at least 32 columns."""
     if world == 1:
         return [("local", pipeline)]
     if not on_gpu:
         return [("torch", "serial")]
     rows = layout == "rows"
-    ipc_ok = rows and rows_per_rank >= 2 * depth
+    ipc_ok = rows_per_rank >= 2 * depth and (rows or (cols_per_rank % 4 == 0 and cols_per_rank >= 32))
     ipc = [("ipc", "auto"), ("ipc", "direct-sys")] if ipc_ok else []
     if not distinct_devices:  # several ranks per GPU: RCCL refuses them; IPC and gloo host staging work
         chain = ipc if transport in ("auto", "ipc") else []

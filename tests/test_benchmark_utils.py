@@ -51,13 +51,15 @@ def test_candidate_chains():
     # ranks sharing one GPU: both direct flavours, then host staging
     assert B.candidates("auto", "auto", 2, True, False, "rows") == [("ipc", "auto"), ("ipc", "direct-sys"),
                                                                     ("host", "serial")]
-    assert B.candidates("auto", "auto", 2, True, False, "blocks") == [("host", "serial")]
+    assert B.candidates("auto", "auto", 4, True, False, "blocks") == [("ipc", "auto"), ("ipc", "direct-sys"),
+                                                                      ("host", "serial")]
+    assert B.candidates("auto", "auto", 4, True, False, "blocks", cols_per_rank=30) == [("host", "serial")]
     # distinct devices (the first cross-device run must fail safe): measured fences, system-scope
     # fences, RCCL signalled, RCCL serial, host staging
     ch = B.candidates("auto", "auto", 8, True, True, "rows")
     assert ch == [("ipc", "auto"), ("ipc", "direct-sys"), ("rccl", "signal"), ("rccl", "serial"), ("host", "serial")]
-    assert B.candidates("auto", "auto", 8, True, True, "blocks") == [("rccl", "signal"), ("rccl", "serial"),
-                                                                     ("host", "serial")]
+    assert B.candidates("auto", "auto", 8, True, True, "blocks") == ch  # 2-D direct IPC too
+    assert B.candidates("auto", "auto", 8, True, True, "blocks", cols_per_rank=4094)[0] == ("rccl", "signal")
     # strips too short for halo units of the depth: no direct IPC candidate
     assert B.candidates("auto", "auto", 8, True, True, "rows", rows_per_rank=10, depth=7)[0] == ("rccl", "signal")
     assert B.candidates("rccl", "serial", 8, True, True, "rows") == [("rccl", "serial"), ("host", "serial")]

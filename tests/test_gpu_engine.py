@@ -203,24 +203,19 @@ def test_rccl_convergence_allreduce(native, gpu):
     assert np.array_equal(eng.download(0), ref["grid"])
 
 
-# pipeline: 0 boundary-first (one stream), 1 concurrent with the boundary units on the comm
-# stream (two streams), 2 concurrent with a boundary stream of its own (three streams),
-# 3 signalled (one launch per chunk, exchange gated mid-kernel by hipStreamWaitValue64),
-# 4 signalled with a polling-kernel gate (the default), 5 the same with the chunk launch waiting on
-# a halo event instead of the in-kernel halo wait, 6 signalled with short boundary units instead
-# of full-size mid-unit-signalling ones
-PIPELINES = {0: dict(concurrent=0, signal_exchange=0), 1: dict(concurrent=1, signal_exchange=0),
-             2: dict(concurrent=1, comm_boundary=0, signal_exchange=0), 3: dict(signal_exchange=1),
-             4: dict(signal_exchange=2), 5: dict(signal_exchange=2, device_halo_wait=0),
-             6: dict(signal_exchange=2, signal_plan=0)}
-PIPELINE_NAMES = {0: "boundary-first", 1: "concurrent", 2: "concurrent3", 3: "signal", 4: "signal", 5: "signal",
-                  6: "signal"}
+# pipeline: 0 serial (exchange, then the chunk), 3 signalled (one launch per chunk, exchange
+# gated mid-kernel by hipStreamWaitValue64), 4 signalled with a polling-kernel gate (the
+# default), 5 the same with the chunk launch waiting on a halo event instead of the in-kernel halo
+# wait, 6 signalled with short boundary units instead of full-size mid-unit-signalling ones
+PIPELINES = {0: dict(overlap=False), 3: dict(signal_exchange=1), 4: dict(signal_exchange=2),
+             5: dict(signal_exchange=2, device_halo_wait=0), 6: dict(signal_exchange=2, signal_plan=0)}
+PIPELINE_NAMES = {0: "serial", 3: "signal", 4: "signal", 5: "signal", 6: "signal"}
 
 
 @pytest.mark.parametrize("gx,gy", [(2, 1), (4, 1), (2, 2), (1, 3)])
-@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("pipeline", [0, 3, 4, 5, 6])
 def test_overlap_pipelines(native, gpu, gx, gy, pipeline):
-    """Boundary-first and concurrent pipelines, with convergence."""
+    """Serial and signalled pipelines (local multi-tile transport), with convergence."""
     nx, ny, steps = 257, 509, 45
     kw = dict(convergence=True, interval=9, sensitivity=1e-30)
     for boundary in (0, 1):
@@ -239,12 +234,12 @@ def test_overlap_pipelines(native, gpu, gx, gy, pipeline):
 
 def test_pipeline_auto(native, gpu):
     assert native.Engine(2048, 2048, gridx=4, gridy=1, device=gpu).pipeline() == "signal"
-    assert native.Engine(2048, 2048, gridx=4, gridy=1, device=gpu, signal_exchange=0).pipeline() == "concurrent"
+    assert native.Engine(2048, 2048, gridx=4, gridy=1, device=gpu, signal_exchange=0).pipeline() == "serial"
     assert native.Engine(2048, 2048, gridx=2, gridy=2, device=gpu, overlap=False).pipeline() == "serial"
     assert native.Engine(2048, 2048, device=gpu).pipeline() == "none"
 
 
-@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("pipeline", [0, 3, 4, 5, 6])
 @pytest.mark.parametrize("contig,comm_cus", [(0, 0), (1, 0), (1, 8), (0, 4)])
 @pytest.mark.parametrize("boundary", [0, 1])
 def test_rccl_self_exchange_row_periodic(native, gpu, pipeline, contig, comm_cus, boundary):
@@ -345,6 +340,48 @@ def test_ipc_direct_self_exchange_row_periodic(native, gpu, nx, ny, boundary, tb
     assert np.array_equal(eng.download(0), ref)
 
 
+@pytest.mark.parametrize("nx,ny", [(96, 300), (300, 704), (257, 4096), (64, 64)])
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("tblock", [8, 5, 16])
+def test_ipc_direct_2d_self_exchange(native, gpu, nx, ny, boundary, tblock):
+    """Periodic in both dimensions, one rank: all eight neighbours are the rank itself, so every
+    halo — rows, W/E ghost columns and the four corners — goes through the 2-D direct protocol
+    (pushes into the ghost-column groups, per-direction flags and counts, K-changing chunks)."""
+    steps = 3 * tblock + 11
+    eng = _ipc_engine(native, nx=nx, ny=ny, periodic_x=True, periodic_y=True, boundary=boundary, tblock=tblock,
+                      device=gpu, poison=True)
+    assert eng.pipeline() == "direct"
+    K = eng.halo_depth()
+    units = eng.unit_list(0, K, 3)
+    assert any(u[7] & 0x3f for u in units)  # side-linked units exist
+    eng.reset_halo_wait()
+    st = eng.run(steps)
+    assert st["steps_done"] == steps
+    ref = oracle(native, nx, ny, steps, boundary, per=(True, True))["grid"]
+    got = eng.download(0)
+    assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
+    assert eng.halo_wait()["waits"] > 0
+    eng.run(7)  # continues the flag sequence (no re-prime)
+    assert np.array_equal(eng.download(0), oracle(native, nx, ny, steps + 7, boundary, per=(True, True))["grid"])
+
+
+def test_ipc_direct_2d_convergence(native, gpu):
+    nx, ny = 96, 300
+    kw = dict(convergence=True, interval=10, sensitivity=1e12)
+    ref = oracle(native, nx, ny, 5000, 1, per=(True, True), **kw)
+    assert ref["converged"]
+    eng = _ipc_engine(native, nx=nx, ny=ny, periodic_x=True, periodic_y=True, boundary=1, device=gpu, **kw)
+    st = eng.run(5000)
+    assert st["converged"] and st["steps_done"] == ref["steps_done"]
+    assert np.array_equal(eng.download(0), ref["grid"])
+
+
+def test_ipc_direct_2d_rejects_unaligned_width(native, gpu):
+    with pytest.raises(Exception, match="multiple of 4"):
+        native.Engine(96, 302, periodic_x=True, periodic_y=True, ranks=[0], transport=native.TRANSPORT_IPC,
+                      device=gpu)
+
+
 @pytest.mark.parametrize("wt", [0, 1])
 @pytest.mark.parametrize("path", ["single", "tiles", "ipc"])
 def test_output_store_policy_bitexact(native, gpu, wt, path):
@@ -380,8 +417,8 @@ def test_ipc_direct_convergence_and_reprime(native, gpu):
 
 
 def test_ipc_direct_rejects_unsupported(native, gpu):
-    with pytest.raises(Exception):
-        native.Engine(96, 300, gridx=1, gridy=2, ranks=[0], transport=native.TRANSPORT_IPC, device=gpu)
+    with pytest.raises(Exception):  # two tiles in one process
+        native.Engine(96, 300, gridx=1, gridy=2, transport=native.TRANSPORT_IPC, device=gpu)
     with pytest.raises(Exception):  # tile too short for full-size halo units
         native.Engine(12, 300, periodic_x=True, ranks=[0], transport=native.TRANSPORT_IPC, device=gpu)
 
@@ -399,7 +436,7 @@ def _gather(eng, nx, ny):
 
 
 @pytest.mark.parametrize("gx,gy", [(1, 1), (2, 1), (1, 2)])
-@pytest.mark.parametrize("pipeline", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("pipeline", [0, 3, 4, 5, 6])
 def test_fused_convergence_matches_oracle(native, gpu, gx, gy, pipeline):
     nx, ny = 257, 509
     ref = oracle(native, nx, ny, 3000, 1, **CONV)

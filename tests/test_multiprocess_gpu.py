@@ -72,6 +72,42 @@ def test_gpu_ranks_ipc_direct_match_oracle(native, gpu, tmp_path, n, boundary, c
     assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
 
 
+@pytest.mark.parametrize("n,gx,gy,boundary,periodic,conv", [(4, 2, 2, "fixed", "none", 0),
+                                                             (8, 2, 4, "ghost-zero", "none", 0),
+                                                             (4, 2, 2, "fixed", "none", 1),
+                                                             (4, 2, 2, "ghost-zero", "xy", 0),
+                                                             (2, 1, 2, "fixed", "none", 0)])
+def test_gpu_ranks_ipc_blocks_match_oracle(native, gpu, tmp_path, n, gx, gy, boundary, periodic, conv):
+    """2-D blocks through the direct pipeline between processes sharing the GPU: row, column and
+    corner halos pushed into the neighbours' IPC-mapped receive buffers, uneven row split,
+    convergence all-reduce."""
+    nx, ny, steps = 61 * gx + 1, 136 * gy, 43
+    args = ["-m", "heat2d_amd", "--device", "gpu", "--transport", "ipc", "--nx", str(nx), "--ny", str(ny),
+            "--steps", str(steps), "--gridx", str(gx), "--gridy", str(gy), "--boundary", boundary, "--periodic",
+            periodic, "--output", "binary", "--outdir", str(tmp_path), "--json"]
+    kw = {}
+    if conv:
+        args += ["--convergence", "1", "--interval", "6", "--sensitivity", "1e-30"]
+        kw = dict(convergence=True, interval=6, sensitivity=1e-30)
+    out = _torchrun(n, args, str(tmp_path))
+    assert '"pipeline": "direct"' in out
+    b = 0 if boundary == "fixed" else 1
+    ref = native.oracle_run(nx, ny, steps, boundary=b, periodic_x="x" in periodic, periodic_y="y" in periodic,
+                            **kw)["grid"]
+    assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
+
+
+def test_gpu_bench_four_ranks_blocks_ipc(tmp_path):
+    """The bench with the 2-D block layout at N=4 on one GPU: the gate picks the 2-D direct
+    pipeline, the timed solver verifies against the oracle and the in-job reference."""
+    out = _torchrun(4, [os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "20", "--warmup", "5", "--side",
+                        "1024", "--layout", "blocks", "--prewarm-s", "0"], str(tmp_path))
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert d["config"]["parallelism"] == "blocks2x2" and d["config"]["candidate"] == "ipc/auto"
+    assert d["config"]["pipeline"] == "direct" and d["verified"] is True
+    assert min(d["halo_wait"]["waits_per_rank"]) > 0
+
+
 def test_gpu_bench_two_ranks_ipc(tmp_path):
     """The bench at N=2 on one GPU: the gate picks the direct IPC transport first."""
     out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "40", "--warmup", "8", "--side",
@@ -122,14 +158,16 @@ def test_gpu_bench_two_ranks_host_transport(tmp_path):
     assert d["gate"][0]["ok"] and d["verified"] is True and d["speedup"] > 0
 
 
-@pytest.mark.parametrize("n,conv", [(2, 0), (3, 1)])
-def test_native_cli_ranks_ipc_on_gpu(native, gpu, tmp_path, n, conv):
-    """The native executable's own launcher (`heat2d --np P`) on the GPU: ranks share the card
-    through the direct IPC halo pipeline; bit-exact against the oracle."""
+@pytest.mark.parametrize("n,gx,conv", [(2, 2, 0), (3, 3, 1), (4, 2, 0)])
+def test_native_cli_ranks_ipc_on_gpu(native, gpu, tmp_path, n, gx, conv):
+    """The native executable's own launcher (`heat2d --np P`, fork without exec) on the GPU:
+    ranks share the card through the direct IPC halo pipeline (rows, and 2x2 blocks);
+    bit-exact against the oracle."""
     exe = os.path.join(ROOT, "heat2d_amd", "bin", "heat2d")
-    nx, ny, steps = 70 * n + 3, 517, 41
+    gy = n // gx
+    nx, ny, steps = 70 * gx + 3, 520 if gy > 1 else 517, 41
     args = [exe, "--np", str(n), "--device", "gpu", "--nx", str(nx), "--ny", str(ny), "--steps", str(steps),
-            "--gridx", str(n), "--gridy", "1", "--output", "binary", "--outdir", str(tmp_path), "--json"]
+            "--gridx", str(gx), "--gridy", str(gy), "--output", "binary", "--outdir", str(tmp_path), "--json"]
     kw = {}
     if conv:
         args += ["--convergence", "1", "--interval", "6", "--sensitivity", "1e-30"]

@@ -26,6 +26,8 @@ for s in "$@"; do
     tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     tests-new) step tests-new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
                  tests/test_gpu_engine.py -k "bench_shape or rank_tiles or timeline" ;;
+    tests-2d) step tests-2d 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+                 tests/test_gpu_engine.py tests/test_multiprocess_gpu.py -k "2d or blocks or native_cli" ;;
     mp) step mp 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_multiprocess_gpu.py ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;
@@ -33,6 +35,8 @@ for s in "$@"; do
     timeline) step timeline 300 python -u tools/timeline.py 4096x4096:7:20 4096x4096:7:70 2048x4096:7:70 \
                 1024x4096:7:70 512x4096:6:60 512x4096:6:60:direct 1024x4096:7:70:direct \
                 --json gpurun_out/timeline.json ;;
+    timeline2) step timeline2 300 python -u tools/timeline.py 512x4096:6:60 512x4096:6:60:direct 1024x4096:7:70 \
+                 8192x4096:7:70 8192x4096:7:70:direct2d 4096x4096:7:70 --json gpurun_out/timeline2.json ;;
     proxy) step proxy 600 python -u tools/strong_proxy.py 4096 840 6,7,8 0 '' 1,2,4,8 ;;
     prof) step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
             python bench.py --steps 20 --warmup 5 --repeat 3 ;;

@@ -4,8 +4,9 @@ For each recorded launch: dispatch spread (first to last wave start), halo wait,
 time (ready -> end) by unit class, launch span, and the gap to the next launch — the parts of
 the per-launch fixed cost that ``profiles/launch_cost_r2.md`` could only fit as one number.
 
-Usage: python tools/timeline.py ROWSxCOLS:K[:steps][:direct] ... [--json out.json]
-  direct = the tile row-periodic through the IPC direct pipeline (its own neighbour).
+Usage: python tools/timeline.py ROWSxCOLS:K[:steps][:direct|direct2d] ... [--json out.json]
+  direct = the tile row-periodic through the IPC direct pipeline (its own neighbour);
+  direct2d = periodic in both dimensions (its own neighbour in all eight directions).
 """
 import json
 import sys
@@ -52,10 +53,13 @@ def run_case(n, spec):
     rows, cols = (int(v) for v in parts[0].split("x"))
     K = int(parts[1])
     steps = int(parts[2]) if len(parts) > 2 and parts[2] else 4 * K
-    direct = len(parts) > 3 and parts[3] == "direct"
+    direct = len(parts) > 3 and parts[3] in ("direct", "direct2d")
     kw = dict(tblock=K, device=0, small_grid_lds=False, tiled=0, timeline=64)
     if direct:
-        e = n.Engine(rows, cols, periodic_x=True, ranks=[0], transport=n.TRANSPORT_IPC, halo_timeout_s=5.0, **kw)
+        # direct2d: periodic in both dimensions — all eight neighbours are the tile itself (the
+        # per-rank shape of a 2-D block decomposition)
+        e = n.Engine(rows, cols, periodic_x=True, periodic_y=parts[3] == "direct2d", ranks=[0],
+                     transport=n.TRANSPORT_IPC, halo_timeout_s=5.0, **kw)
         e.ipc_open([e.ipc_handle()])
         e.ipc_prime()
     else:
