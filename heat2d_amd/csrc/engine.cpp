@@ -1103,9 +1103,26 @@ RunStats Engine::run_impl(int64_t steps) {
     // chunk length (TY = RY - 2k).
     st.path = "tiled";
     Tile& T = tiles_[0];
+    // A lone fused-check tile lets a chunk run THROUGH a check step: the residual is summed at
+    // that level inside the launch (TileArgs::rlev) and a converged check is rolled back by
+    // recomputation, so a check costs no launch of its own (interval 20 at K 16: 1.25 launches
+    // per 20 steps instead of 2).
+    const bool span = fused_ && recompute_rollback();
     while (steps_done_ < target) {
       bool check = false;
-      const int k = chunk_len(steps_done_, target, tile_k_, &check);
+      int lvl = 0;
+      int k;
+      if (span) {
+        const int64_t seg = target - steps_done_, n = (seg + tile_k_ - 1) / tile_k_;
+        const int64_t next_check = (steps_done_ / opt_.interval + 1) * opt_.interval;
+        int64_t kk = std::max<int64_t>(1, (seg + n - 1) / n);
+        kk = std::min<int64_t>(kk, next_check + opt_.interval - 1 - steps_done_);  // one check per chunk
+        k = (int)kk;
+        check = opt_.convergence && steps_done_ + k >= next_check;
+        lvl = check ? (int)(next_check - steps_done_) : 0;
+      } else {
+        k = chunk_len(steps_done_, target, tile_k_, &check);
+      }
       TileArgs a;
       a.src = T.buf[T.cur] + T.g.idx(0, 0);
       a.dst = T.buf[1 - T.cur] + T.g.idx(0, 0);
@@ -1128,6 +1145,7 @@ RunStats Engine::run_impl(int64_t steps) {
         a.stop = d_stop_;
         if (check) {
           a.keep = recompute_rollback() ? nullptr : T.keep + T.g.idx(0, 0);
+          a.rlev = lvl;
           a.dec = decide_args(0, true);  // the last block sums the partials and decides
           decided_in_launch_ = true;
         }
@@ -1140,7 +1158,7 @@ RunStats Engine::run_impl(int64_t steps) {
       ++st.chunks;
       if (check) {
         if (fused_) {
-          if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+          if (check_point(steps_done_, k, lvl > 0 ? lvl : k)) break;  // converged (seen by the host)
         } else {
           st.residual = finish_residual();
           if (st.residual < opt_.sensitivity) {
@@ -1354,12 +1372,13 @@ void Engine::device_decide(unsigned long long seq) {
   }
 }
 
-bool Engine::check_point(int64_t steps_before, int k) {
+bool Engine::check_point(int64_t steps_before, int k, int lvl) {
   // The chunk just enqueued ended on a check step: record it, enqueue the decision, and tell
   // the caller whether the host already sees a converged check (then it stops enqueueing;
   // launches queued after the converged one are no-ops on the device).
   const unsigned long long seq = ++chunk_seq_;
-  checks_.push_back(CheckRec{seq, steps_before, k, 1 - tiles_[0].cur});  // cur has flipped past the chunk
+  // cur has flipped past the chunk; lvl: the check's level in the chunk (k: its last)
+  checks_.push_back(CheckRec{seq, steps_before, k, 1 - tiles_[0].cur, lvl > 0 ? lvl : k});
   if (!decided_in_launch_) device_decide(seq);
   decided_in_launch_ = false;
   if (rccl_comm_) {
@@ -1381,7 +1400,7 @@ bool Engine::finalize_convergence(RunStats& st) {
     if (it == checks_.end()) throw std::logic_error("converged check not found");
     // the result is the state one step before the converged check (B-5): the level K-1 rows
     // the check launch kept
-    steps_done_ = it->steps_before + it->k - 1;
+    steps_done_ = it->steps_before + it->lvl - 1;
     st.converged = true;
     st.residual = h_conv_->residual;
     H2D_HIP_CHECK(hipMemsetAsync(d_stop_, 0, sizeof(unsigned long long), compute_));
@@ -1389,8 +1408,8 @@ bool Engine::finalize_convergence(RunStats& st) {
       // the launches after the converged check were no-ops, so the check chunk's input buffer
       // still holds the state at steps_before: advance it k-1 steps (plain launches, no check)
       tiles_[0].cur = it->src;
-      launched = it->k > 1;
-      for (int left = it->k - 1; left > 0;) {
+      launched = it->lvl > 1;
+      for (int left = it->lvl - 1; left > 0;) {
         int kk = std::min(left, G_);
         while (kk > 1 && !stream_k_supported(kk)) --kk;
         advance(kk, false);
@@ -1631,6 +1650,7 @@ Engine::IpcLayout Engine::ipc_layout_of(int rank) const {
   if (side) {
     // W / E ghost-column groups (kGhostGroup columns per side and parity) in rows [-G, xcell+G),
     // with the tile's pitch (the streaming kernel's ghost lanes read them like tile rows)
+    if (g.pitch < 4 * IpcLayout::kGroupStride) throw std::logic_error("IPC layout: pitch too small for the groups");
     L.xbuf = off;
     off += (((size_t)(g.xcell + 2 * g.G) * (size_t)g.pitch * sizeof(float)) + 4095) & ~size_t(4095);
   }

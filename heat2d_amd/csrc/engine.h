@@ -331,8 +331,12 @@ class Engine {
     size_t xbuf = 0;     // W / E ghost-column groups (2-D blocks only; 0: none)
     int64_t pitch = 0;   // the tile's row pitch (floats): also the xbuf's
     size_t bytes = 0;
-    // group (side 0 W / 1 E, parity p): its column 0 in xbuf row 0 (= tile row -G)
-    size_t group(int side, int p) const { return xbuf + (size_t)(2 * side + p) * kGhostGroup * sizeof(float); }
+    // group (side 0 W / 1 E, parity p): its column 0 in xbuf row 0 (= tile row -G).  Each group
+    // has a 256-byte segment of its own in every row (rows start 256-byte aligned): the parity a
+    // chunk reads never shares a cache line with the parity its pushes write (measured: with the
+    // groups packed 64 bytes apart, ghost columns read stale values under concurrent pushes).
+    static constexpr int kGroupStride = 64;  // floats
+    size_t group(int side, int p) const { return xbuf + (size_t)(2 * side + p) * kGroupStride * sizeof(float); }
   };
   static constexpr int kIpcMaxRanks = 64;
   IpcLayout ipc_layout_of(int rank) const;
@@ -358,6 +362,7 @@ class Engine {
     int64_t steps_before;
     int k;
     int src;  // the check chunk's input buffer (tile 0): unchanged by the no-op launches after it
+    int lvl;  // the check step's level in the chunk (== k unless the chunk runs through the check)
   };
   // A lone single-process tile keeps no rollback copy in its check launches: on convergence
   // the state one step before the check is recomputed from the check chunk's input (k-1 steps).
@@ -371,7 +376,7 @@ class Engine {
   int last_nparts_ = 0;
   DecideArgs decide_args(int t, bool decide) const;
   void device_decide(unsigned long long seq);
-  bool check_point(int64_t steps_before, int k);
+  bool check_point(int64_t steps_before, int k, int lvl = 0);
   bool finalize_convergence(RunStats& st);  // true: it enqueued recompute launches
   double ipc_allreduce_residual();
   void* rccl_comm_ = nullptr;       // ncclComm_t

@@ -21,6 +21,10 @@ struct TileArgs {
   double* partials;  // [ntiles] residual partials (residual launches)
   const unsigned long long* stop = nullptr;  // converged earlier: the launch does nothing
   float* keep = nullptr;  // residual launches: level K-1 of the owned tile (rollback state)
+  // residual launches: the level whose change is summed (the convergence check step inside the
+  // chunk; 0 = the last level K).  With rlev < K the launch goes on to level K, and a converged
+  // check is rolled back by recomputation (keep must be null).
+  int rlev = 0;
   DecideArgs dec;         // residual launches: fused sum + decision (last block)
 };
 size_t tile_lds_bytes(int TX, int RY, int K);

@@ -187,8 +187,9 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
     }
   }
 
+  const int rlev = a.rlev > 0 ? a.rlev : K;
   for (int t = 1; t <= K; ++t) {
-    const bool last = t == K;
+    const bool last = t == rlev;  // the residual's level (the check step of the chunk)
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
       if (j * RSTEP >= RX - t) break;  // uniform: no lane has a j-th row at this level
@@ -279,6 +280,8 @@ bool tile_config_ok(int TX, int RY, int K, int CPL, int NT) {
 void launch_tile(TileArgs a, int precision, bool residual, hipStream_t s) {
   if (!tile_config_ok(a.TX, a.RY, a.K, a.CPL, a.NT)) throw std::invalid_argument("launch_tile: bad tile configuration");
   if (a.TY != a.RY - 2 * a.K) throw std::invalid_argument("launch_tile: TY must be RY - 2K");
+  if (a.rlev < 0 || a.rlev > a.K || (a.rlev != 0 && a.rlev != a.K && a.keep != nullptr))
+    throw std::invalid_argument("launch_tile: residual level outside the chunk (or with a rollback copy)");
   if (a.NT != 256 && a.NT != 1024) throw std::invalid_argument("launch_tile: NT must be 256 or 1024");
   a.tiles_y = (a.NY + a.TY - 1) / a.TY;
   a.ntiles = ((a.NX + a.TX - 1) / a.TX) * a.tiles_y;

@@ -63,9 +63,9 @@ def test_phase_trace(native, gpu, signal_exchange):
     eng = native.Engine(512, 1024, gridx=2, device=gpu, trace=True, signal_exchange=signal_exchange)
     st = eng.run(40)
     ph = st["phase_ms"]
-    # signalled pipeline: one launch per chunk; split pipelines: interior + boundary launches
-    main = "chunk" if eng.pipeline() == "signal" else "interior"
-    assert ({"chunk", "exchange"} if main == "chunk" else {"boundary", "interior", "exchange"}) <= set(ph), ph
+    # signalled pipeline: one launch per chunk; serial pipeline: exchange, then the chunk's step
+    main = "chunk" if eng.pipeline() == "signal" else "step"
+    assert {main, "exchange"} <= set(ph), ph
     assert all(v >= 0 for v in ph.values())
     assert st["phase_count"][main] == st["chunks"]
 

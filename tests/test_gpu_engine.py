@@ -468,6 +468,24 @@ def test_fused_convergence_intervals(native, gpu, interval, tblock):
     assert np.array_equal(eng.download(0), ref["grid"])
 
 
+@pytest.mark.parametrize("interval,tile_k", [(20, 16), (9, 16), (7, 6), (1, 8), (16, 16), (33, 16)])
+def test_tiled_chunks_run_through_checks(native, gpu, interval, tile_k):
+    """Tiled lone tile with the fused check: chunks span check steps (the residual is summed at
+    the check's level inside the launch), a converged check is rolled back by recomputation —
+    same converged step and grid as the oracle, and fewer launches than one-chunk-per-check."""
+    nx, ny = 257, 509
+    for sens in (2.68e13, 0.0):  # converges (after a few checks) / never converges
+        kw = dict(convergence=True, interval=interval, sensitivity=sens)
+        ref = oracle(native, nx, ny, 400, 1, **kw)
+        eng = native.Engine(nx, ny, boundary=1, device=gpu, tiled=1, tile_k=tile_k, small_grid_lds=False, **kw)
+        st = eng.run(400)
+        assert st["path"] == "tiled" and st["converged"] == ref["converged"]
+        assert st["steps_done"] == ref["steps_done"], (st, ref["steps_done"])
+        assert np.array_equal(eng.download(0), ref["grid"])
+        if not ref["converged"]:
+            assert st["chunks"] <= -(-400 // tile_k) + 400 // max(interval, tile_k) + 1
+
+
 def test_fused_convergence_tiled_and_split_runs(native, gpu):
     nx, ny = 257, 509
     ref = oracle(native, nx, ny, 3000, 1, **CONV)

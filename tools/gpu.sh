@@ -26,6 +26,8 @@ for s in "$@"; do
     tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     tests-new) step tests-new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
                  tests/test_gpu_engine.py -k "bench_shape or rank_tiles or timeline" ;;
+    tests-no2d) step tests-no2d 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+                 -k "not 2d and not blocks" ;;
     tests-2d) step tests-2d 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
                  tests/test_gpu_engine.py tests/test_multiprocess_gpu.py -k "2d or blocks or native_cli" ;;
     mp) step mp 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_multiprocess_gpu.py ;;
@@ -37,6 +39,7 @@ for s in "$@"; do
                 --json gpurun_out/timeline.json ;;
     timeline2) step timeline2 300 python -u tools/timeline.py 512x4096:6:60 512x4096:6:60:direct 1024x4096:7:70 \
                  8192x4096:7:70 8192x4096:7:70:direct2d 4096x4096:7:70 --json gpurun_out/timeline2.json ;;
+    diag2d) step diag2d 400 python -u tools/diag2d.py 257 4096 5 3 ;;
     proxy) step proxy 600 python -u tools/strong_proxy.py 4096 840 6,7,8 0 '' 1,2,4,8 ;;
     prof) step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
             python bench.py --steps 20 --warmup 5 --repeat 3 ;;

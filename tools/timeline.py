@@ -4,7 +4,7 @@ For each recorded launch: dispatch spread (first to last wave start), halo wait,
 time (ready -> end) by unit class, launch span, and the gap to the next launch — the parts of
 the per-launch fixed cost that ``profiles/launch_cost_r2.md`` could only fit as one number.
 
-Usage: python tools/timeline.py ROWSxCOLS:K[:steps][:direct|direct2d] ... [--json out.json]
+Usage: python tools/timeline.py ROWSxCOLS:K[:steps][:alone|direct|direct2d[:opt=value...]] ... [--json out.json]
   direct = the tile row-periodic through the IPC direct pipeline (its own neighbour);
   direct2d = periodic in both dimensions (its own neighbour in all eight directions).
 """
@@ -55,6 +55,9 @@ def run_case(n, spec):
     steps = int(parts[2]) if len(parts) > 2 and parts[2] else 4 * K
     direct = len(parts) > 3 and parts[3] in ("direct", "direct2d")
     kw = dict(tblock=K, device=0, small_grid_lds=False, tiled=0, timeline=64)
+    for extra in parts[4:]:  # engine options, name=value (e.g. direct_acquire=2)
+        name, value = extra.split("=")
+        kw[name] = int(value)
     if direct:
         # direct2d: periodic in both dimensions — all eight neighbours are the tile itself (the
         # per-rank shape of a 2-D block decomposition)
