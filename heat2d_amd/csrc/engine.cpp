@@ -328,6 +328,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       }
     }
     if (!opt_.naive) warm_stream_kernels(opt_.precision, G_, compute_);
+    if (!opt_.naive && opt_.persistent != 0) warm_pstream_kernels(opt_.precision, G_, compute_);
     if (tiled_) warm_tile_kernels(opt_.precision, compute_);
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
   }
@@ -348,6 +349,10 @@ Engine::~Engine() {
   if (d_ticket_) hipFree(d_ticket_);
   if (h_conv_) hipHostFree(h_conv_);
   if (ev_check_) hipEventDestroy(ev_check_);
+  for (auto& kv : pplans_) {
+    hipFree(kv.second.d_units);
+    hipFree(kv.second.d_prog);
+  }
   for (auto& kv : units_) {
     hipFree(kv.second.d_all);
     hipFree(kv.second.d_interior);
@@ -1203,6 +1208,29 @@ RunStats Engine::run_impl(int64_t steps) {
       bool check = false;
       int k = next_chunk(steps_done_, target, &check);
       while (k > 0) {
+        if (!check) {
+          const int J = plain_run(steps_done_, target, k);
+          if (J >= 2 && pplan(k) != nullptr) {
+            // a run of equal plain chunks: ONE persistent launch (the same flags, counts and
+            // receive-buffer parities per chunk as the launches below)
+            trace_begin("chunk", compute_);
+            launch_pstream_chunks(k, J);
+            trace_end("chunk", compute_);
+            for (int d = 0; d < kNumDirs; ++d) {
+              const int pr = dec_.neighbor(tiles_[0].rank, d);
+              if (pr >= 0)
+                ipc_need_[d] += (unsigned long long)J * (unsigned long long)ipc_counts_[pr].at((size_t)k * kNumDirs + kDirOpp[d]);
+            }
+            ipc_chunk_ += (unsigned long long)J;
+            if (J & 1) tiles_[0].cur = 1 - tiles_[0].cur;
+            st.chunks += J;
+            st.exchanges += J;
+            poll_abort();
+            steps_done_ += (int64_t)J * k;
+            k = next_chunk(steps_done_, target, &check);
+            continue;
+          }
+        }
         trace_begin("chunk", compute_);
         launch_chunk_tile(0, k, check, 3);
         trace_end("chunk", compute_);
@@ -1295,6 +1323,20 @@ RunStats Engine::run_impl(int64_t steps) {
       while (steps_done_ < target) {
         bool check = false;
         const int k = next_chunk(steps_done_, target, &check);
+        if (!has_exchange_ && !check && !opt_.naive) {
+          // a run of equal plain chunks: ONE persistent launch
+          const int J = plain_run(steps_done_, target, k);
+          if (J >= 2 && pplan(k) != nullptr) {
+            trace_begin("step", compute_);
+            launch_pstream_chunks(k, J);
+            trace_end("step", compute_);
+            if (J & 1) tiles_[0].cur = 1 - tiles_[0].cur;
+            st.chunks += J;
+            steps_done_ += (int64_t)J * k;
+            poll_abort();
+            continue;
+          }
+        }
         if (has_exchange_) {
           H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
           H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
@@ -1331,6 +1373,141 @@ RunStats Engine::run_impl(int64_t steps) {
   trace_collect(st);
   st.steps_done = steps_done_;
   return st;
+}
+
+// ---- persistent pipelined stencil ----------------------------------------------------------
+
+int Engine::plain_run(int64_t done, int64_t target, int k) const {
+  // consecutive chunks of depth k without a check, starting at `done` (capped: a launch of at
+  // most 256 chunks, so the host still polls for device-side failures now and then)
+  int J = 0;
+  while (J < 256 && done < target) {
+    bool check = false;
+    const int kk = next_chunk(done, target, &check);
+    if (kk != k || check) break;
+    done += kk;
+    ++J;
+  }
+  return J;
+}
+
+const Engine::PPlan* Engine::pplan(int K) {
+  auto it = pplans_.find(K);
+  if (it != pplans_.end()) return it->second.n > 0 ? &it->second : nullptr;
+  PPlan P;
+  const bool ok_path = on_gpu() && !opt_.naive && !tiled_ && opt_.persistent != 0 && tiles_.size() == 1 &&
+                       K <= kMaxPK && K <= G_ && stream_k_supported(K) && !fused_;
+  const Tile& T = tiles_[0];
+  const TileGeom& g = T.g;
+  bool halo_n = false, halo_s = false, ok = ok_path;
+  if (ok && has_exchange_) {
+    // only the direct pipeline of 1-D row strips (no west / east / corner neighbours)
+    ok = direct_;
+    for (int d = kW; d < kNumDirs && ok; ++d) ok = dec_.neighbor(T.rank, d) < 0;
+    halo_n = dec_.neighbor(T.rank, kN) >= 0;
+    halo_s = dec_.neighbor(T.rank, kS) >= 0;
+  }
+  // write-through stores and 32-bit row offsets (as launch_chunk_tile's a.wt)
+  if (ok) ok = (opt_.wt_store < 0 ? 1 : opt_.wt_store) != 0 &&
+               (double)(g.xcell + 2 * g.G) * (double)g.pitch * sizeof(float) < 2147483648.0 - 1048576.0;
+  if (ok) {
+    const int64_t cap = (int64_t)device_cus_ * 4;  // one wave per SIMD, every wave resident
+    const int bpc = pstream_blocks_per_cu(K, opt_.precision);
+    P.host = plan_pstream(g, K, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
+                          opt_.row_edge_weight > 0 ? opt_.row_edge_weight : opt_.edge_weight, cap, halo_n, halo_s,
+                          std::max(K, G_));
+    P.n = (int)P.host.size();
+    if (P.n == 0 || bpc < 1 || (P.n + 3) / 4 > (int64_t)device_cus_ * bpc) P.n = 0;
+    if (P.n > 0 && has_exchange_) {
+      // a chunk must push exactly as often as the neighbours' launch-per-chunk plan says
+      const UnitLists& L = units(0, K);
+      int pn = 0, ps = 0;
+      for (const PUnit& u : P.host)
+        if (u.u.flags & kUnitNS) ((u.u.flags & kUnitReverse) ? ps : pn)++;
+      if ((halo_n && pn != L.pushes[kN]) || (halo_s && ps != L.pushes[kS])) P.n = 0;
+    }
+  }
+  if (P.n > 0) {
+    P.d_units = dmalloc<PUnit>((size_t)P.n);
+    H2D_HIP_CHECK(hipMemcpy(P.d_units, P.host.data(), (size_t)P.n * sizeof(PUnit), hipMemcpyHostToDevice));
+    P.d_prog = dmalloc<unsigned>((size_t)P.n * 32);
+    H2D_HIP_CHECK(hipMemset(P.d_prog, 0, (size_t)P.n * 32 * sizeof(unsigned)));
+  }
+  auto& ref = pplans_.emplace(K, std::move(P)).first->second;
+  return ref.n > 0 ? &ref : nullptr;
+}
+
+void Engine::launch_pstream_chunks(int K, int J) {
+  PPlan& P = pplans_.at(K);
+  Tile& T = tiles_[0];
+  const TileGeom& g = T.g;
+  PStreamArgs a;
+  a.units = P.d_units;
+  a.nunits = P.n;
+  a.nchunks = J;
+  a.cbase = P.cdone;
+  a.buf[0] = T.buf[0];
+  a.buf[1] = T.buf[1];
+  a.cur0 = T.cur;
+  a.src0 = T.buf[T.cur];
+  a.prog = P.d_prog;
+  a.pitch = g.pitch;
+  a.G = g.G;
+  a.PL = g.PL;
+  a.xcell = g.xcell;
+  a.ycell = g.ycell;
+  a.gx0 = g.gx0;
+  a.gy0 = g.gy0;
+  a.NX = g.NX;
+  a.NY = g.NY;
+  a.cx = opt_.cx;
+  a.cy = opt_.cy;
+  a.fixed = opt_.boundary == kFixed;
+  a.dummy = d_dummy_;
+  a.halo_polls = std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6));
+  a.timed_out = d_sig_timeout_;
+  a.timed_out_host = h_timeout_dev_;
+  a.wait_acc = d_wait_acc_;
+  if (direct_) {
+    const int64_t rowb = g.pitch * (int64_t)sizeof(float);
+    const IpcLayout& me = ipc_lays_[T.rank];
+    const int pn = dec_.neighbor(T.rank, kN), ps = dec_.neighbor(T.rank, kS);
+    if (pn >= 0) {
+      const IpcLayout& nl = ipc_lays_[pn];
+      a.wait[0] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kN]);
+      a.need0[0] = ipc_need_[kN];
+      a.need_inc[0] = (unsigned long long)ipc_counts_[pn].at((size_t)K * kNumDirs + kS);
+      a.sig[0] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pn] + nl.flag[kS]);
+      for (int p = 0; p < 2; ++p) {
+        a.hsrc[0][p] = reinterpret_cast<const float*>(ipc_block_ + me.recv_n[p]);
+        a.push[0][p] = reinterpret_cast<float*>(ipc_blocks_[pn] + nl.recv_s[p]);
+      }
+    }
+    if (ps >= 0) {
+      const IpcLayout& sl = ipc_lays_[ps];
+      a.wait[1] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kS]);
+      a.need0[1] = ipc_need_[kS];
+      a.need_inc[1] = (unsigned long long)ipc_counts_[ps].at((size_t)K * kNumDirs + kN);
+      a.sig[1] = reinterpret_cast<unsigned long long*>(ipc_blocks_[ps] + sl.flag[kN]);
+      for (int p = 0; p < 2; ++p) {
+        a.hsrc[1][p] = reinterpret_cast<const float*>(ipc_block_ + me.recv_s[p] - (g.G + g.xcell) * rowb);
+        a.push[1][p] = reinterpret_cast<float*>(ipc_blocks_[ps] + sl.recv_n[p] - (g.xcell - g.G) * rowb);
+      }
+    }
+    a.ipar0 = (int)(ipc_chunk_ & 1);
+    a.sig_rows = G_;
+    a.rel = opt_.direct_release < 0 ? 2 : opt_.direct_release;
+    a.acq = opt_.direct_acquire < 0 ? 1 : opt_.direct_acquire;
+  }
+  launch_pstream(a, K, opt_.precision, compute_);
+  P.cdone += (unsigned)J;
+  ++pstream_launches_;
+  progress_tick(compute_);
+}
+
+std::vector<PUnit> Engine::pstream_units(int K) {
+  const PPlan* P = pplan(K);
+  return P ? P->host : std::vector<PUnit>();
 }
 
 // ---- device-side convergence (fused check) -----------------------------------------------

@@ -89,6 +89,10 @@ struct EngineOptions {
   int direct_acquire = -1;
   // Streaming kernel output rows: 0 plain stores, 1 write-through (sc1), -1 the measured default.
   int wt_store = -1;
+  // Persistent pipelined stencil (pstream_kernel.hpp): runs of >= 2 equal plain chunks in ONE
+  // launch on an aligned unit grid (single tile without exchange, or the direct IPC pipeline of
+  // row strips).  -1 auto, 0 off, 1 on.
+  int persistent = -1;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
   // Diagnostics: record the per-wave timeline (s_memrealtime stamps) of the first `timeline`
@@ -222,6 +226,9 @@ class Engine {
   std::vector<LaunchTimeline> timeline() const;
   // The work units of tile t at depth K in launch order (which: 0 all, 3 halo units first).
   std::vector<Unit> unit_list(int t, int K, int which);
+  // The persistent plan's units at depth K (empty: no persistent launch at this depth).
+  std::vector<PUnit> pstream_units(int K);
+  int64_t pstream_launches() const { return pstream_launches_; }
 
  private:
   struct Tile {
@@ -351,6 +358,19 @@ class Engine {
   unsigned long long ipc_chunk_ = 0;        // chunks since the prime (receive-buffer parity)
   unsigned long long ipc_need_[kNumDirs] = {};  // halo pushes expected from each direction (cumulative)
   unsigned long long ipc_resid_epoch_ = 0;  // residual all-reduces since the prime
+  // ---- persistent pipelined stencil ----
+  struct PPlan {
+    PUnit* d_units = nullptr;
+    unsigned* d_prog = nullptr;  // progress words, 32 apart
+    int n = 0;
+    unsigned cdone = 0;          // chunks run by this plan's launches (progress base)
+    std::vector<PUnit> host;
+  };
+  std::map<int, PPlan> pplans_;  // by K (an empty plan: not eligible)
+  int64_t pstream_launches_ = 0;
+  const PPlan* pplan(int K);     // build / look up; nullptr if depth K runs launch per chunk
+  int plain_run(int64_t done, int64_t target, int k) const;  // equal plain chunks of depth k from `done`
+  void launch_pstream_chunks(int K, int J);
   // ---- device-side convergence ----
   bool fused_ = false;
   unsigned long long* d_stop_ = nullptr;  // 0 running, else the sequence number of the converged check

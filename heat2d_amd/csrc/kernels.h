@@ -173,6 +173,63 @@ struct StreamArgs {
   unsigned long long* stamps = nullptr;
 };
 
+// ---- persistent pipelined streaming stencil (pstream_kernel.hpp) ---------------------------
+// ONE launch runs J chunks of depth K.  Every wave keeps its unit for the whole launch; units
+// sit on an aligned grid (every column strip cut at the same row bands, band i streaming down
+// for even i and up for odd i), and a unit starts chunk j as soon as the rows its K-cone reads
+// from its eight neighbours' chunk j-1 outputs are published — no kernel boundary, no grid-wide
+// drain: a unit's first rows of a chunk are what the bands above / below need first.
+// Progress words: unit w publishes prog[32 w] = (chunks done) * h + (rows of the current chunk
+// whose write-through stores have completed), monotonically across the plan's launches.
+constexpr int kPSlots = 8;  // neighbour slots: above, below, left, right, and the four diagonals
+struct PUnit {
+  Unit u;  // geometry as for the streaming kernel (links unused)
+  int band;
+  // per slot: neighbour unit (-1: none); my stream rows [rlo, rhi) come from its outputs; its
+  // output index of my stream row r is qa + qs * r (qs = +-1); its rows per chunk hv
+  int nb[kPSlots], rlo[kPSlots], rhi[kPSlots], qa[kPSlots], qs[kPSlots], hv[kPSlots];
+};
+struct PStreamArgs {
+  const PUnit* units;
+  int nunits;
+  int nchunks;          // J (>= 1)
+  unsigned cbase;       // chunks this plan completed in earlier launches (progress base)
+  const float* src0;    // buffer read by chunk 0 (chunk j reads buf[(cur0 + j) & 1])
+  float* buf[2];
+  int cur0;
+  unsigned* prog;       // progress words, 32 apart (one 128-B line each)
+  int64_t pitch, G, PL;
+  int64_t xcell, ycell;
+  int64_t gx0, gy0, NX, NY;
+  double cx, cy;
+  int fixed;
+  float* dummy;
+  // direct (IPC) halo units, per direction (0 north / top band, 1 south / bottom band, reverse)
+  // and receive-buffer parity: chunk j reads parity (ipar0 + j) & 1 and pushes to the other
+  const unsigned long long* wait[2] = {nullptr, nullptr};
+  unsigned long long need0[2] = {0, 0}, need_inc[2] = {0, 0};
+  const float* hsrc[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  float* push[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  unsigned long long* sig[2] = {nullptr, nullptr};
+  int ipar0 = 0;
+  int sig_rows = 0;
+  int rel = 2, acq = 1;
+  long long halo_polls = 0;
+  unsigned int* timed_out = nullptr;
+  unsigned int* timed_out_host = nullptr;
+  unsigned long long* wait_acc = nullptr;
+};
+// Largest K with a compiled persistent kernel (K <= 8, write-through stores).
+constexpr int kMaxPK = 8;
+void launch_pstream(const PStreamArgs& a, int K, int precision, hipStream_t s);
+// Resident 256-thread blocks per CU of the persistent kernel (every block must be resident).
+int pstream_blocks_per_cu(int K, int precision);
+void warm_pstream_kernels(int precision, int kmax, hipStream_t s);
+// The aligned unit grid of the persistent kernel (empty if the tile does not allow one):
+// `bands` row bands (even when both halo directions exist), every band at least hmin rows.
+std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x, bool per_y, double row_edge_weight,
+                                int64_t capacity, bool halo_n, bool halo_s, int hmin);
+
 // Largest K with a compiled streaming kernel.
 constexpr int kMaxK = 16;
 bool stream_k_supported(int K);
@@ -222,4 +279,8 @@ template <int K, bool F32, bool RESID>
 void launch_stream_kv(const StreamArgs& a, hipStream_t s);
 template <int K, bool F32, bool RESID>
 int stream_blocks_per_cu_v();
+template <int K, bool F32>
+void launch_pstream_kv(const PStreamArgs& a, hipStream_t s);
+template <int K, bool F32>
+int pstream_blocks_per_cu_v();
 }  // namespace h2d

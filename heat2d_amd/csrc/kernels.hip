@@ -509,6 +509,150 @@ void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hip
   H2D_HIP_CHECK(hipGetLastError());
 }
 
+// ---- persistent pipelined variant (pstream_kernel.hpp, generated TUs pstream_k<K>_f<F>.hip) ----
+#define H2D_PK_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+#define H2D_PEXTERN(K)                                                              \
+  extern template void launch_pstream_kv<K, false>(const PStreamArgs&, hipStream_t); \
+  extern template void launch_pstream_kv<K, true>(const PStreamArgs&, hipStream_t);  \
+  extern template int pstream_blocks_per_cu_v<K, false>();                           \
+  extern template int pstream_blocks_per_cu_v<K, true>();
+H2D_PK_LIST(H2D_PEXTERN)
+#undef H2D_PEXTERN
+
+void launch_pstream(const PStreamArgs& a, int K, int precision, hipStream_t s) {
+  const bool f32 = precision == kFp32;
+  switch (K) {
+#define H2D_CASE(KK) \
+  case KK: f32 ? launch_pstream_kv<KK, true>(a, s) : launch_pstream_kv<KK, false>(a, s); break;
+    H2D_PK_LIST(H2D_CASE)
+#undef H2D_CASE
+    default: throw std::invalid_argument("no persistent stencil compiled for K=" + std::to_string(K));
+  }
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+int pstream_blocks_per_cu(int K, int precision) {
+  const bool f32 = precision == kFp32;
+  switch (K) {
+#define H2D_CASE(KK) \
+  case KK: return f32 ? pstream_blocks_per_cu_v<KK, true>() : pstream_blocks_per_cu_v<KK, false>();
+    H2D_PK_LIST(H2D_CASE)
+#undef H2D_CASE
+    default: return 0;
+  }
+}
+
+void warm_pstream_kernels(int precision, int kmax, hipStream_t s) {
+  PStreamArgs a{};
+  a.nunits = 0;
+  for (int K = 1; K <= std::min(kmax, kMaxPK); ++K) launch_pstream(a, K, precision, s);
+}
+
+std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x, bool per_y, double row_edge_weight,
+                                int64_t capacity, bool halo_n, bool halo_s, int hmin) {
+  std::vector<PUnit> out;
+  const std::vector<Strip> strips = strip_layout(g, K, fixed, per_y);
+  const int S = (int)strips.size();
+  if (S < 1 || capacity < S) return out;
+  hmin = std::max(hmin, K);  // a K-cone spans at most the adjacent bands
+  // bands: as many as one wave per SIMD allows; even when the bottom band must stream up (a
+  // south halo: its ghost rows come first in its stream)
+  int m = (int)std::min<int64_t>(capacity / S, g.xcell / hmin);
+  if (halo_s && (m & 1)) --m;
+  if (m < 1 || (halo_s && m < 2)) return out;
+  // band heights: equal cost (h + K) * w, row-edge bands (their cone reaches a global edge row)
+  // weighted w = row_edge_weight
+  const double wr = std::max(1.0, row_edge_weight);
+  std::vector<int64_t> a0, hh;
+  for (;;) {
+    std::vector<double> w(m, 1.0);
+    auto row_edge = [&](int64_t lo, int64_t hi) {  // rows [lo, hi) of the tile, cone K
+      return (unit_edge_flags(g, K, lo, hi - lo, strips[S / 2].cb, fixed, per_x, true) & kEdgeRows) != 0;
+    };
+    // first estimate with equal bands, then the weights of the bands at the tile's edge rows
+    const int64_t eq = g.xcell / m;
+    if (row_edge(0, eq)) w[0] = wr;
+    if (row_edge(g.xcell - eq, g.xcell)) w[m - 1] = wr;
+    double inv = 0.0;
+    for (double x : w) inv += 1.0 / x;
+    const double U = ((double)g.xcell + (double)m * K) / inv;
+    a0.assign(m + 1, 0);
+    hh.assign(m, 0);
+    double acc = 0.0;
+    for (int i = 0; i < m; ++i) {
+      acc += U / w[i] - K;
+      a0[i + 1] = (i == m - 1) ? g.xcell : std::min<int64_t>(g.xcell, (int64_t)std::llround(acc));
+    }
+    bool ok = true;
+    for (int i = 0; i < m; ++i) {
+      hh[i] = a0[i + 1] - a0[i];
+      if (hh[i] < hmin) ok = false;
+    }
+    if (ok) break;
+    m -= halo_s ? 2 : 1;
+    if (m < 1 || (halo_s && m < 2)) return {};
+  }
+  auto uidx = [&](int band, int strip) { return band * S + strip; };
+  out.resize((size_t)m * S);
+  for (int i = 0; i < m; ++i) {
+    for (int s = 0; s < S; ++s) {
+      PUnit& p = out[(size_t)uidx(i, s)];
+      const Strip& st = strips[(size_t)s];
+      p.u = Unit{s, (int)a0[i], (int)hh[i], unit_edge_flags(g, K, a0[i], hh[i], st.cb, fixed, per_x, per_y),
+                 (int)st.cb, (int)st.lo, (int)st.hi, 0};
+      if (i & 1) p.u.flags |= kUnitReverse;
+      if ((i == 0 && halo_n) || (i == m - 1 && halo_s)) p.u.flags |= kUnitNS;
+      p.band = i;
+    }
+  }
+  // neighbour slots: 0 above, 1 below, 2 left, 3 right, 4 above-left, 5 above-right,
+  // 6 below-left, 7 below-right
+  static const int kDb[kPSlots] = {-1, 1, 0, 0, -1, -1, 1, 1};
+  static const int kDs[kPSlots] = {0, 0, -1, 1, -1, 1, -1, 1};
+  for (int i = 0; i < m; ++i)
+    for (int s = 0; s < S; ++s) {
+      PUnit& p = out[(size_t)uidx(i, s)];
+      const int64_t x0 = a0[i], h = hh[i];
+      const bool rev = (i & 1) != 0;
+      const int64_t wlo = strips[(size_t)s].cb, whi = wlo + kWaveCols;  // my column window
+      // a window must not reach past the adjacent strips' outputs
+      for (int s2 = 0; s2 < S; ++s2)
+        if (std::abs(s2 - s) > 1 && strips[(size_t)s2].lo < whi && strips[(size_t)s2].hi > wlo) return {};
+      for (int l = 0; l < kPSlots; ++l) {
+        p.nb[l] = -1;
+        p.rlo[l] = p.rhi[l] = p.qa[l] = p.qs[l] = p.hv[l] = 0;
+        const int i2 = i + kDb[l], s2 = s + kDs[l];
+        if (i2 < 0 || i2 >= m || s2 < 0 || s2 >= S) continue;
+        const Strip& t = strips[(size_t)s2];
+        if (!(t.lo < whi && t.hi > wlo)) continue;  // no column of its outputs in my window
+        const int64_t a2 = a0[i2], h2 = hh[i2];
+        const bool rev2 = (i2 & 1) != 0;
+        const int64_t tlo = std::max(a2, x0 - K), thi = std::min(a2 + h2, x0 + h + K);  // tile rows
+        if (tlo >= thi) continue;
+        int64_t rlo, rhi, qa, qs;
+        if (!rev) {
+          rlo = tlo - (x0 - K);
+          rhi = thi - (x0 - K);
+        } else {
+          rlo = x0 + h + K - thi;
+          rhi = x0 + h + K - tlo;
+        }
+        // my stream row r -> tile row T(r) -> its output index q(T)
+        if (!rev && !rev2) qa = x0 - K - a2, qs = 1;
+        else if (!rev && rev2) qa = a2 + h2 - 1 - x0 + K, qs = -1;
+        else if (rev && !rev2) qa = x0 + h + K - 1 - a2, qs = -1;
+        else qa = a2 + h2 - x0 - h - K, qs = 1;
+        p.nb[l] = uidx(i2, s2);
+        p.rlo[l] = (int)rlo;
+        p.rhi[l] = (int)rhi;
+        p.qa[l] = (int)qa;
+        p.qs[l] = (int)qs;
+        p.hv[l] = (int)h2;
+      }
+    }
+  return out;
+}
+
 void warm_stream_kernels(int precision, int kmax, hipStream_t s) {
   StreamArgs a{};
   a.nunits = 0;

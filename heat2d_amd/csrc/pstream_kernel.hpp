@@ -1,0 +1,313 @@
+// heat2d_amd — persistent, pipelined variant of the streaming stencil (gfx950).
+//
+// The launch-per-chunk streaming kernel (stream_kernel.hpp) pays, per chunk, a dependent kernel
+// boundary (~1.4 us), the dispatch and unit-record load (~0.8 us), and a cold start of every
+// wave: its 2K prologue rows all arrive one memory round trip after the launch, and its last
+// stores drain before the grid ends (measured with the per-wave timeline: ~3.3 us of fixed
+// body time per unit).  At 512 x 4096 per GPU (4096^2 over 8 GPUs) that is ~40 % of a launch.
+//
+// Here ONE launch runs J chunks.  Every wave keeps its work unit; units form an aligned grid
+// (all column strips cut at the same row bands), band i streams DOWN for even i and UP for odd
+// i, so the rows a unit's K-cone needs first from the band above / below are the rows that
+// band produces FIRST.  A unit starts chunk j as soon as the rows it is about to load from its
+// eight neighbours' chunk j-1 outputs are published — per row, not per grid.
+//
+// Hand-off (MI355X guide, Guideline 16 R1 / visibility table row 1): every output row is
+// stored write-through (buffer_store sc1); a wave publishes "rows complete" in its own progress
+// word with an agent-scope atomic store only after an `s_waitcnt vmcnt(8)` at a steady-loop
+// iteration top — every store issued before the previous top has completed, so the publication
+// lags one iteration and never stalls; consumers poll progress words with relaxed agent loads
+// (one vector load: lane l reads neighbour slot l) and read tile rows with sc1 buffer loads
+// only (L1 bypass), so no acquire fence is needed.  The polls are issued one iteration ahead;
+// a wave stalls only if a neighbour really is behind.
+//
+// Direct (IPC) halo units keep the launch-per-chunk protocol per chunk: wait on the flag, read
+// ghost rows from the receive buffer of the chunk's parity, push the first G output rows into
+// the neighbour's buffer of the other parity and signal once those stores have completed.
+//
+// Deadlock freedom: a unit publishes everything it has completed before every wait, and chunk
+// j's outputs never depend on chunk j+1, so by induction over j every wait is eventually met.
+// Every launch's waves must all be resident (the host checks occupancy); every wait is bounded
+// and reports through the engine's timeout words.
+#pragma once
+#include "stream_kernel.hpp"
+
+namespace h2d {
+namespace {
+
+// sc1 (L1-bypassing, coherent for write-through hand-offs) 16-byte row load of one lane.
+__device__ __forceinline__ float4 load_row_sc1(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 16 /* sc1 */);
+  return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
+}
+
+// Lane l < kPSlots holds neighbour slot l; other lanes are inert (nb < 0).
+struct PSlot {
+  int nb, rlo, rhi, qa, qs, hv;
+  unsigned known;  // latest progress seen
+};
+
+// Progress the rows [A, B) of my stream need from this lane's neighbour (its chunk cprev).
+__device__ __forceinline__ unsigned pneed(const PSlot& d, int A, int B, unsigned cprev) {
+  const int lo = max(A, d.rlo), hi = min(B, d.rhi);
+  if (d.nb < 0 || lo >= hi) return 0u;
+  const int r = d.qs > 0 ? hi - 1 : lo;
+  return cprev * (unsigned)d.hv + (unsigned)(d.qa + d.qs * r + 1);
+}
+
+__device__ __forceinline__ unsigned ppoll(const PSlot& d, const unsigned* prog) {
+  return d.nb >= 0 ? __hip_atomic_load(prog + 32 * d.nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
+}
+
+// Wait until every neighbour has published what rows [A, B) need (bounded).  false: gave up.
+__device__ __forceinline__ bool pensure(PSlot& d, int A, int B, unsigned cprev, const unsigned* prog,
+                                        const PStreamArgs& a, bool& dead) {
+  const unsigned nd = pneed(d, A, B, cprev);
+  if (dead || __ballot(nd > d.known) == 0ull) return true;
+  for (long long i = 0;; ++i) {
+    const unsigned v = ppoll(d, prog);
+    d.known = max(d.known, v);
+    if (__ballot(nd > d.known) == 0ull) return true;
+    if (i > a.halo_polls ||
+        ((i & 63) == 63 && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+      if (__lane_id() == 0) report_timeout(a.timed_out, a.timed_out_host, 8u);
+      dead = true;
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ void ppublish(unsigned* p, unsigned v, int lane) {
+  if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The direct pipeline's flag signal of a halo unit (its pushed rows' stores have completed).
+__device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int lane) {
+  if (rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  else if (rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (rel != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int K, bool F32, int EDGE, bool FIXED>
+__device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w, int lane, PSlot& sl) {
+  const int h = u.h, n = h + 2 * K;
+  const bool rev = (u.flags & kUnitReverse) != 0;
+  const bool ns = (u.flags & kUnitNS) != 0;
+  const int dir = rev ? 1 : 0;
+  const int64_t x0 = u.x0;
+  const int64_t cb = (int64_t)u.cb + 4 * lane;
+  const int64_t xin = rev ? x0 + h - 1 + K : x0 - K;
+  const int64_t xout = rev ? x0 + h - 1 : x0;
+  const int pb = (int)(a.pitch * (int64_t)sizeof(float));  // row bytes (the host keeps n * pb < 2^31)
+  const Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
+  unsigned* myprog = a.prog + 32 * w;
+
+  // chunk-invariant lane context (stream_kernel's, write-through stores, no residual / sides)
+  LaneCtx c;
+  c.gxb = a.gx0 + xin;
+  c.dir = rev ? -1 : 1;
+  c.NX = a.NX;
+  const int64_t gc = a.gy0 + cb;
+  auto colmask = [&](int64_t q) { return a.fixed ? (q == 0 || q == a.NY - 1) : (q < 0 || q >= a.NY); };
+  c.m0 = colmask(gc + 0);
+  c.m1 = colmask(gc + 1);
+  c.m2 = colmask(gc + 2);
+  c.m3 = colmask(gc + 3);
+  const bool in_out = (cb >= u.olo) && (cb < u.ohi);
+  c.sout = a.dummy + 4 * lane;  // unused: write-through path
+  c.spitch = 0;
+  c.obs = rev ? -pb : pb;
+  c.obo = rev ? (h - 1) * pb : 0;
+  c.voff = in_out ? 16u * (unsigned)lane : 0x80000000u;
+  c.st0 = c.st1 = c.st2 = c.st3 = false;
+  c.kout = a.dummy + 4 * lane;
+  c.kpitch = 0;
+  c.rel = a.rel;
+  c.spu = false;
+  c.em = 0u;
+  c.sp = c.cn = c.cs = nullptr;
+  c.sps = c.cns = c.css = 0;
+  c.xr0 = xout;
+  c.xdir = rev ? -1 : 1;
+  c.xlo = a.G;
+  c.xhi = a.xcell - a.G;
+  const bool pushes = ns && a.push[dir][0] != nullptr;
+  c.prows = pushes ? a.sig_rows : 0;
+  const int64_t in_base = (a.G + x0 - K) * a.pitch + a.PL + u.cb;  // lowest input row, lane 0
+  const int64_t out_base = (a.G + x0) * a.pitch + a.PL + u.cb;     // lowest output row, lane 0
+  const int64_t lane_in = (a.G + xin) * a.pitch + a.PL + cb;       // first stream row, this lane
+  const int64_t pitch4 = rev ? -(a.pitch >> 2) : (a.pitch >> 2);
+  const unsigned lvoff = 16u * (unsigned)lane;
+  auto soff = [&](int r) { return rev ? (n - 1 - r) * pb : r * pb; };
+
+  bool dead = false;         // a wait gave up: finish without waiting (the host reports it)
+  bool sig_pending = false;  // a halo unit's pushes of its last chunk are not yet signalled
+  double racc = 0.0;
+  for (int j = 0; j < a.nchunks; ++j) {
+    const unsigned cidx = a.cbase + (unsigned)j;
+    const int par = (a.cur0 + j) & 1;
+    const float* src = a.buf[par];
+    float* dst = a.buf[par ^ 1];
+    const int ipar = (a.ipar0 + j) & 1;
+    if (j > 0) {
+      // chunk start: my previous chunk's stores complete (the poll's wait drains them), publish
+      // them, then the rows the up-front batch loads must be published by the neighbours
+      const unsigned pv = ppoll(sl, a.prog);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ppublish(myprog, cidx * (unsigned)h, lane);
+      if (sig_pending) {
+        psignal(a.sig[dir], a.rel, lane);
+        sig_pending = false;
+      }
+      sl.known = max(sl.known, pv);
+      pensure(sl, 0, min(n, 2 * K + 4), cidx - 1u, a.prog, a, dead);
+    }
+    const float4* hrowp = nullptr;
+    if (ns && a.wait[dir] != nullptr) {
+      // the neighbour GPU's pushes of its chunk j-1 (this chunk's ghost rows)
+      if (lane == 0 && !dead && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+        const unsigned long long need = a.need0[dir] + (unsigned long long)j * a.need_inc[dir];
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        long long i = 0;
+        while (__hip_atomic_load(a.wait[dir], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
+          if (++i > a.halo_polls) {
+            report_timeout(a.timed_out, a.timed_out_host, 2u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (a.wait_acc != nullptr) {
+          const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+          __hip_atomic_fetch_add(a.wait_acc, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(a.wait_acc + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_max(a.wait_acc + 2, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (a.acq == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      else if (a.acq == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      hrowp = reinterpret_cast<const float4*>(a.hsrc[dir][ipar] + lane_in);
+    }
+    c.obase = dst + out_base;
+    c.pout = (pushes && in_out) ? a.push[dir][ipar ^ 1] + xout * a.pitch + a.PL + cb : a.dummy + 4 * lane;
+    c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
+    const __amdgpu_buffer_rsrc_t rin =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src) + in_base, (short)0, n * pb, 0x00020000);
+
+    float4 S[K][2];
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      S[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      S[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 pro[2 * K];
+#pragma unroll
+    for (int i = 0; i < 2 * K; ++i) pro[i] = (i < K && hrowp != nullptr) ? hrowp[(int64_t)i * pitch4]
+                                                                        : load_row_sc1(rin, lvoff, soff(i));
+    float4 pf[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) pf[d] = load_row_sc1(rin, lvoff, soff(min(2 * K + d, n - 1)));
+    __builtin_amdgcn_sched_barrier(0);
+    prologue<K, F32, EDGE, FIXED, false, true, false, 0>(S, pro, c, k, racc);
+
+    int ir0 = 2 * K;
+    int issued_prev = 0;  // output rows issued before the previous iteration top
+    bool signalled = false;
+    unsigned polled = 0u;
+    bool have_poll = false;
+#define H2D_PSTEADY(D)                                                                \
+  {                                                                                   \
+    const float4 nw = pf[D];                                                          \
+    pf[D] = load_row_sc1(rin, lvoff, soff(min(ir0 + (D) + 4, n - 1)));                \
+    process_row<K, F32, EDGE, FIXED, false, true, false, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
+  }
+    for (; ir0 + 4 <= n; ir0 += 4) {
+      // iteration top: every op before the previous top has completed (>= 8 VMEM ops since)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);
+      if (pushes && !signalled && issued_prev >= a.sig_rows) {  // the pushed rows have completed
+        psignal(a.sig[dir], a.rel, lane);
+        signalled = true;
+      }
+      if (have_poll) sl.known = max(sl.known, polled);
+      polled = ppoll(sl, a.prog);  // consumed at the next top
+      have_poll = true;
+      issued_prev = ir0 - 2 * K;
+      if (j > 0) pensure(sl, ir0 + 4, min(n, ir0 + 8), cidx - 1u, a.prog, a, dead);
+      H2D_PSTEADY(0)
+      H2D_PSTEADY(1)
+      H2D_PSTEADY(2)
+      H2D_PSTEADY(3)
+    }
+#undef H2D_PSTEADY
+    if (ir0 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[0], ir0, c, k, racc);
+    if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
+    if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
+    if (have_poll) sl.known = max(sl.known, polled);
+    // pushes not yet signalled at an iteration top: at the next chunk start (or launch end)
+    if (pushes && !signalled) sig_pending = true;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ppublish(myprog, (a.cbase + (unsigned)a.nchunks) * (unsigned)h, lane);
+  if (sig_pending) psignal(a.sig[dir], a.rel, lane);
+}
+
+template <int K, bool F32>
+__global__ __launch_bounds__(256) void pstream_kernel(PStreamArgs a) {
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int w = (int)blockIdx.x * 4 + wv;
+  if (w >= a.nunits) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const PUnit* pu = a.units + w;
+  const Unit u = pu->u;
+  PSlot sl;
+  if (lane < kPSlots) {
+    sl.nb = pu->nb[lane];
+    sl.rlo = pu->rlo[lane];
+    sl.rhi = pu->rhi[lane];
+    sl.qa = pu->qa[lane];
+    sl.qs = pu->qs[lane];
+    sl.hv = pu->hv[lane];
+  } else {
+    sl.nb = -1;
+    sl.rlo = sl.rhi = sl.qa = sl.qs = sl.hv = 0;
+  }
+  sl.known = 0u;
+  const bool fixed = a.fixed != 0;
+  switch (u.flags & 3) {
+    case 0: prun<K, F32, 0, false>(a, u, w, lane, sl); break;
+    case 1:
+      if (fixed) prun<K, F32, 1, true>(a, u, w, lane, sl);
+      else prun<K, F32, 1, false>(a, u, w, lane, sl);
+      break;
+    case 2:
+      if (fixed) prun<K, F32, 2, true>(a, u, w, lane, sl);
+      else prun<K, F32, 2, false>(a, u, w, lane, sl);
+      break;
+    default:
+      if (fixed) prun<K, F32, 3, true>(a, u, w, lane, sl);
+      else prun<K, F32, 3, false>(a, u, w, lane, sl);
+      break;
+  }
+}
+
+}  // namespace
+
+template <int K, bool F32>
+void launch_pstream_kv(const PStreamArgs& a, hipStream_t s) {
+  const int blocks = std::max(1, (a.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_pstream_kernels)
+  hipLaunchKernelGGL((pstream_kernel<K, F32>), dim3(blocks), dim3(256), 0, s, a);
+}
+
+template <int K, bool F32>
+int pstream_blocks_per_cu_v() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(pstream_kernel<K, F32>), 256,
+                                                   0) != hipSuccess)
+    return 0;
+  return nb;
+}
+
+}  // namespace h2d

@@ -186,7 +186,7 @@ def test_host_sanitizers_engine_cpu_path(native, tmp_path):
     drv.write_text(ENGINE_SAN_DRIVER)
     srcs = [str(drv)] + [os.path.join(csrc, f) for f in ("engine.cpp", "decomposition.cpp", "cpu_reference.cpp",
                                                           "kernels.hip")]
-    prebuilt = [_build._obj_for(f) for f in ["tile_kernel.hip"] + list(_build.STREAM_TUS)]
+    prebuilt = [_build._obj_for(f) for f in ["tile_kernel.hip"] + list(_build.GEN_TUS)]
     assert all(os.path.exists(o) for o in prebuilt)
     flags = ["-x", "hip", "--offload-arch=gfx950", "-std=c++17", "-O1", "-ffp-contract=off", f"-I{csrc}",
              "-Xarch_host", "-g", "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",

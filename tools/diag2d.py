@@ -25,14 +25,15 @@ def ranges(v):
     return ",".join(out)
 
 
-for poison in (True, False):
+order = sys.argv[5] if len(sys.argv) > 5 else "pf"
+for poison in [c == "p" for c in order]:
     for rep in range(reps):
         e = n.Engine(nx, ny, periodic_x=True, periodic_y=True, boundary=1, tblock=tb, device=0, ranks=[0],
                      transport=n.TRANSPORT_IPC, halo_timeout_s=5.0, poison=poison)
         e.ipc_open([e.ipc_handle()])
         e.ipc_prime()
         K0, _ = e.next_chunk(0, steps)
-        if rep == 0 and poison:
+        if rep == 0:
             units = e.unit_list(0, K0, 3)
             print(f"K={K0} units={len(units)} halo={sum(1 for u in units if (u[3] & 16) or u[7])}")
             last = max(u[0] for u in units)

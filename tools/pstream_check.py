@@ -1,0 +1,73 @@
+"""Persistent pipelined stencil: bit-exactness against the oracle and us/step against the
+launch-per-chunk kernel, alone and through the row-periodic direct IPC pipeline (the per-rank
+shape of 4096^2 strong scaling).
+
+Usage: python tools/pstream_check.py [check] [time]"""
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from heat2d_amd._native import native  # noqa: E402
+
+n = native()
+what = set(sys.argv[1:]) or {"check", "time"}
+
+
+def engine(nx, ny, K, pers, direct=False, **kw):
+    if direct:
+        e = n.Engine(nx, ny, periodic_x=True, tblock=K, device=0, ranks=[0], transport=n.TRANSPORT_IPC,
+                     halo_timeout_s=5.0, persistent=pers, **kw)
+        e.ipc_open([e.ipc_handle()])
+        e.ipc_prime()
+        return e
+    return n.Engine(nx, ny, tblock=K, device=0, small_grid_lds=False, tiled=0, persistent=pers, halo_timeout_s=5.0, **kw)
+
+
+if "check" in what:
+    for nx, ny, K, steps, boundary, direct in [(300, 517, 7, 37, 0, False), (300, 517, 6, 36, 1, False),
+                                               (512, 4096, 6, 60, 0, False), (257, 1000, 4, 41, 1, False),
+                                               (96, 300, 5, 3 * 5 + 11, 0, True), (512, 4096, 6, 60, 0, True),
+                                               (1024, 4096, 7, 70, 1, True), (300, 701, 8, 37, 1, True),
+                                               (2048, 4096, 7, 140, 0, False)]:
+        e = engine(nx, ny, K, 1, direct=direct, boundary=boundary, poison=True)
+        st = e.run(steps)
+        got = e.download(0)
+        ref = n.oracle_run(nx, ny, steps, boundary=boundary, periodic_x=direct)["grid"]
+        d = got != ref
+        r, c = np.nonzero(d)
+        print(f"check {nx}x{ny} K={K} steps={steps} b={boundary} direct={direct}: launches {e.pstream_launches()} "
+              f"chunks {st['chunks']} wrong {int(d.sum())}"
+              + (f" rows {r.min()}-{r.max()} cols {c.min()}-{c.max()} nan {int(np.isnan(got).sum())}" if d.any() else ""),
+              flush=True)
+        # continue: a second run (new launch, progress counters continue)
+        e.run(steps)
+        ref2 = n.oracle_run(nx, ny, 2 * steps, boundary=boundary, periodic_x=direct)["grid"]
+        print(f"   second run: wrong {int((e.download(0) != ref2).sum())}", flush=True)
+        del e
+
+
+def timed(e, steps, reps=5):
+    e.run(steps)
+    best = 1e9
+    for _ in range(reps):
+        e.synchronize()
+        t0 = time.perf_counter()
+        e.run(steps)
+        e.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    return best / steps * 1e6
+
+
+if "time" in what:
+    for nx, ny, K, steps in [(512, 4096, 6, 840), (1024, 4096, 7, 840), (2048, 4096, 7, 840), (4096, 4096, 7, 840),
+                             (4096, 4096, 7, 20), (512, 4096, 6, 24)]:
+        for direct in (False, True):
+            row = []
+            for pers in (0, 1):
+                e = engine(nx, ny, K, pers, direct=direct)
+                row.append(timed(e, steps))
+                del e
+            print(f"time {nx}x{ny} K={K} steps={steps} direct={direct}: per-chunk {row[0]:.3f} us/step, "
+                  f"persistent {row[1]:.3f} us/step ({row[0] / row[1]:.3f}x)", flush=True)
