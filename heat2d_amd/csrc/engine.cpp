@@ -1395,10 +1395,17 @@ const Engine::PPlan* Engine::pplan(int K) {
   auto it = pplans_.find(K);
   if (it != pplans_.end()) return it->second.n > 0 ? &it->second : nullptr;
   PPlan P;
-  const bool ok_path = on_gpu() && !opt_.naive && !tiled_ && opt_.persistent != 0 && tiles_.size() == 1 &&
-                       K <= kMaxPK && K <= G_ && stream_k_supported(K) && !fused_;
   const Tile& T = tiles_[0];
   const TileGeom& g = T.g;
+  // auto: only where one launch per chunk is measurably the bottleneck — the direct pipeline's
+  // short per-rank strips (tools/pstream_check.py on MI355X, us/step over 840 steps, per-chunk vs
+  // persistent: 512x4096 K=6 2.475 vs 2.112, 1024x4096 K=7 3.176 vs 2.873, 2048x4096 4.706 vs
+  // 4.800, 4096^2 7.743 vs 8.816; a lone tile: 512x4096 2.162 vs 2.101, 1024 3.173 vs 3.328,
+  // 4096^2 7.744 vs 9.207 — profiles/pstream_r3.txt).  Timeline runs stamp per-chunk launches.
+  const bool want = opt_.persistent > 0 ||
+                    (opt_.persistent < 0 && direct_ && has_exchange_ && g.xcell <= 1536 && opt_.timeline == 0 && K >= 2);
+  const bool ok_path = on_gpu() && !opt_.naive && !tiled_ && want && tiles_.size() == 1 && K <= kMaxPK && K <= G_ &&
+                       stream_k_supported(K) && !fused_;
   bool halo_n = false, halo_s = false, ok = ok_path;
   if (ok && has_exchange_) {
     // only the direct pipeline of 1-D row strips (no west / east / corner neighbours)

@@ -81,7 +81,9 @@ def test_gpu_ranks_ipc_blocks_match_oracle(native, gpu, tmp_path, n, gx, gy, bou
     """2-D blocks through the direct pipeline between processes sharing the GPU: row, column and
     corner halos pushed into the neighbours' IPC-mapped receive buffers, uneven row split,
     convergence all-reduce."""
-    nx, ny, steps = 61 * gx + 1, 136 * gy, 43
+    # tiles of 600 columns: a strip that pushes to a W/E neighbour must not also hold a global
+    # edge column (the engine refuses narrower tiles at a global edge)
+    nx, ny, steps = 61 * gx + 1, 600 * gy, 43
     args = ["-m", "heat2d_amd", "--device", "gpu", "--transport", "ipc", "--nx", str(nx), "--ny", str(ny),
             "--steps", str(steps), "--gridx", str(gx), "--gridy", str(gy), "--boundary", boundary, "--periodic",
             periodic, "--output", "binary", "--outdir", str(tmp_path), "--json"]

@@ -28,6 +28,7 @@ for s in "$@"; do
     diagconv2) step diagconv2 300 python -u tools/diag_conv2.py ;;
     diagconv2b) HIP_LAUNCH_BLOCKING=1 step diagconv2b 300 python -u tools/diag_conv2.py ;;
     diagconv) step diagconv 300 python -u tools/diag_conv.py ;;
+    tests-k) step tests-k 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf -k "$TESTK" ;;
     tests-new) step tests-new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
                  tests/test_gpu_engine.py -k "bench_shape or rank_tiles or timeline" ;;
     tests-no2d) step tests-no2d 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
@@ -35,6 +36,8 @@ for s in "$@"; do
     tests-2d) step tests-2d 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
                  tests/test_gpu_engine.py tests/test_multiprocess_gpu.py -k "2d or blocks or native_cli" ;;
     mp) step mp 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_multiprocess_gpu.py ;;
+    pcheck) step pcheck 300 python -u tools/pstream_check.py check ;;
+    ptime) step ptime 300 python -u tools/pstream_check.py time ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench1000) step bench1000 300 python bench.py --steps 1000 --warmup 200 ;;

@@ -30,9 +30,18 @@ if "check" in what:
                                                (512, 4096, 6, 60, 0, False), (257, 1000, 4, 41, 1, False),
                                                (96, 300, 5, 3 * 5 + 11, 0, True), (512, 4096, 6, 60, 0, True),
                                                (1024, 4096, 7, 70, 1, True), (300, 701, 8, 37, 1, True),
-                                               (2048, 4096, 7, 140, 0, False)]:
+                                               (2048, 4096, 7, 140, 0, False), (203, 611, 1, 5, 0, False),
+                                               (203, 611, 2, 7, 0, False), (203, 611, 3, 9, 1, False),
+                                               (64, 611, 1, 5, 0, False), (512, 611, 1, 5, 0, False)]:
         e = engine(nx, ny, K, 1, direct=direct, boundary=boundary, poison=True)
-        st = e.run(steps)
+        units = e.pstream_units(K)
+        hs = sorted({u[2] for u in units})
+        print(f"  plan: {len(units)} units, h {hs[:3]}..{hs[-3:]}" if units else "  plan: none", flush=True)
+        try:
+            st = e.run(steps)
+        except RuntimeError as ex:
+            print(f"check {nx}x{ny} K={K}: FAILED {ex}", flush=True)
+            continue
         got = e.download(0)
         ref = n.oracle_run(nx, ny, steps, boundary=boundary, periodic_x=direct)["grid"]
         d = got != ref
