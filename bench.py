@@ -135,11 +135,12 @@ def main() -> int:
             side = B.fill_hbm_side(int(ctx.allreduce_min(free)), G=a.tblock)
     nx, ny, gx, gy = B.grid_for(world, side, scaling, layout)
     ref_tblock = a.tblock  # depth of the in-job single-GPU reference (a whole grid / one tile)
-    if user_tblock <= 0 and a.precision == "ref" and nx // gx <= 1024:
-        # short per-rank tiles (4096^2 over >= 4 GPUs): the K-cone of ~9-17-row units favours 6
-        # (512x4096 alone: 20 steps 2.99 vs 3.12 us/step, 840 steps 2.01 vs 2.20; 1024 rows equal;
-        # 2048 rows 7 is best: profiles/small_tile_k_r2.txt)
-        a.tblock = 6
+    if user_tblock <= 0 and a.precision == "ref" and world > 1 and nx // gx <= 1024:
+        # short per-rank tiles (4096^2 over >= 4 GPUs) run the persistent kernel through the direct
+        # pipeline, whose fixed cost is per chunk: depth 8 is best there (512x4096 row-periodic,
+        # us/step over 840 steps, K 6/7/8: 2.179/2.059/2.034; 1024 rows 2.963/2.869/2.870 —
+        # profiles/pstream_r3.txt)
+        a.tblock = 8
 
     def config(nx_, ny_, steps_, transport, pipeline, gridx, gridy, conv=False):
         c = Config(preset="heat2d", nx=nx_, ny=ny_, steps=steps_, gridx=gridx, gridy=gridy, boundary=a.boundary,

@@ -318,7 +318,7 @@ class Solver:
                                   tiles=res.ntiles, path=res.path, converged=res.converged,
                                   residual=res.residual, device="gpu" if self.on_gpu else "cpu",
                                   precision=c.precision, boundary=c.boundary, tblock=self.engine.halo_depth(),
-                                  chunks=res.chunks, exchanges=res.exchanges))
+                                  chunks=res.chunks, exchanges=res.exchanges, pipeline=self.engine.pipeline()))
         return res
 
     def save(self, path: str) -> None:

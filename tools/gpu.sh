@@ -38,6 +38,8 @@ for s in "$@"; do
     mp) step mp 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_multiprocess_gpu.py ;;
     pcheck) step pcheck 300 python -u tools/pstream_check.py check ;;
     ptime) step ptime 300 python -u tools/pstream_check.py time ;;
+    convtable) step convtable 600 python -u tools/conv_table.py ;;
+    pksweep) step pksweep 300 python -u tools/pstream_check.py ksweep ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench1000) step bench1000 300 python bench.py --steps 1000 --warmup 200 ;;

@@ -80,3 +80,15 @@ if "time" in what:
                 del e
             print(f"time {nx}x{ny} K={K} steps={steps} direct={direct}: per-chunk {row[0]:.3f} us/step, "
                   f"persistent {row[1]:.3f} us/step ({row[0] / row[1]:.3f}x)", flush=True)
+
+if "ksweep" in what:
+    # halo depth = chunk depth K, direct row-periodic pipeline (the per-rank shape of strong scaling)
+    for nx in (512, 1024):
+        for K in (2, 3, 4, 5, 6, 7, 8):
+            row = []
+            for pers in (0, 1):
+                e = engine(nx, 4096, K, pers, direct=True)
+                row.append(timed(e, 840))
+                del e
+            print(f"ksweep {nx}x4096 K={K} direct: per-chunk {row[0]:.3f} us/step, persistent {row[1]:.3f} us/step",
+                  flush=True)
