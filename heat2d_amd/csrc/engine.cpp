@@ -328,7 +328,8 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       }
     }
     if (!opt_.naive) warm_stream_kernels(opt_.precision, G_, compute_);
-    if (!opt_.naive && opt_.persistent != 0) warm_pstream_kernels(opt_.precision, G_, compute_);
+    if (!opt_.naive && (opt_.persistent > 0 || (opt_.persistent < 0 && direct_)))
+      warm_pstream_kernels(opt_.precision, G_, compute_);
     if (tiled_) warm_tile_kernels(opt_.precision, compute_);
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
   }
@@ -1210,16 +1211,16 @@ RunStats Engine::run_impl(int64_t steps) {
       while (k > 0) {
         if (!check) {
           const int J = plain_run(steps_done_, target, k);
-          if (J >= 2 && pplan(k) != nullptr) {
-            // a run of equal plain chunks: ONE persistent launch (the same flags, counts and
-            // receive-buffer parities per chunk as the launches below)
+          if (J >= 2 && pst_everywhere(k) && pplan(k) != nullptr) {
+            // a run of equal plain chunks: ONE persistent launch (the same flags and receive-
+            // buffer parities per chunk as the launches below; every rank's plan has a
+            // persistent plan at this depth, so every rank runs this chunk run the same way)
             trace_begin("chunk", compute_);
             launch_pstream_chunks(k, J);
             trace_end("chunk", compute_);
-            for (int d = 0; d < kNumDirs; ++d) {
+            for (int d = kN; d <= kS; ++d) {  // 1-D row strips: N / S neighbours only
               const int pr = dec_.neighbor(tiles_[0].rank, d);
-              if (pr >= 0)
-                ipc_need_[d] += (unsigned long long)J * (unsigned long long)ipc_counts_[pr].at((size_t)k * kNumDirs + kDirOpp[d]);
+              if (pr >= 0) ipc_need_[d] += (unsigned long long)J * (unsigned long long)pst_counts_[pr].at((size_t)k * 2 + (d == kN ? 1 : 0));
             }
             ipc_chunk_ += (unsigned long long)J;
             if (J & 1) tiles_[0].cur = 1 - tiles_[0].cur;
@@ -1418,21 +1419,21 @@ const Engine::PPlan* Engine::pplan(int K) {
   if (ok) ok = (opt_.wt_store < 0 ? 1 : opt_.wt_store) != 0 &&
                (double)(g.xcell + 2 * g.G) * (double)g.pitch * sizeof(float) < 2147483648.0 - 1048576.0;
   if (ok) {
+    // strip width: 128 columns for short tiles (twice the unit height at the same wave count:
+    // the K-cone (K-1)/h halves), else 256 (profiles/pstream_r3.txt, us/step 256 vs 128 columns,
+    // K=8: 512x4096 2.077 vs 1.908; 1024 rows 2.867 vs 3.031; 2048 rows 4.789 vs 5.157)
+    P.cpl = opt_.pstream_cols == 256 ? 4 : opt_.pstream_cols == 128 ? 2 : (g.xcell <= 768 ? 2 : 4);
     const int64_t cap = (int64_t)device_cus_ * 4;  // one wave per SIMD, every wave resident
-    const int bpc = pstream_blocks_per_cu(K, opt_.precision);
+    const int bpc = pstream_blocks_per_cu(K, opt_.precision, P.cpl);
     P.host = plan_pstream(g, K, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                           opt_.row_edge_weight > 0 ? opt_.row_edge_weight : opt_.edge_weight, cap, halo_n, halo_s,
-                          std::max(K, G_));
+                          std::max(K, G_), P.cpl);
     P.n = (int)P.host.size();
     if (P.n == 0 || bpc < 1 || (P.n + 3) / 4 > (int64_t)device_cus_ * bpc) P.n = 0;
-    if (P.n > 0 && has_exchange_) {
-      // a chunk must push exactly as often as the neighbours' launch-per-chunk plan says
-      const UnitLists& L = units(0, K);
-      int pn = 0, ps = 0;
-      for (const PUnit& u : P.host)
-        if (u.u.flags & kUnitNS) ((u.u.flags & kUnitReverse) ? ps : pn)++;
-      if ((halo_n && pn != L.pushes[kN]) || (halo_s && ps != L.pushes[kS])) P.n = 0;
-    }
+    // N / S halo units: each adds 1 to the neighbour's flag per chunk (the neighbours learn the
+    // count from the IPC handle, Engine::ipc_handle)
+    for (const PUnit& u : P.host)
+      if (u.u.flags & kUnitNS) ++P.pushes[(u.u.flags & kUnitReverse) ? 1 : 0];
   }
   if (P.n > 0) {
     P.d_units = dmalloc<PUnit>((size_t)P.n);
@@ -1483,7 +1484,7 @@ void Engine::launch_pstream_chunks(int K, int J) {
       const IpcLayout& nl = ipc_lays_[pn];
       a.wait[0] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kN]);
       a.need0[0] = ipc_need_[kN];
-      a.need_inc[0] = (unsigned long long)ipc_counts_[pn].at((size_t)K * kNumDirs + kS);
+      a.need_inc[0] = (unsigned long long)pst_counts_[pn].at((size_t)K * 2 + 1);  // N's south pushes
       a.sig[0] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pn] + nl.flag[kS]);
       for (int p = 0; p < 2; ++p) {
         a.hsrc[0][p] = reinterpret_cast<const float*>(ipc_block_ + me.recv_n[p]);
@@ -1494,7 +1495,7 @@ void Engine::launch_pstream_chunks(int K, int J) {
       const IpcLayout& sl = ipc_lays_[ps];
       a.wait[1] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kS]);
       a.need0[1] = ipc_need_[kS];
-      a.need_inc[1] = (unsigned long long)ipc_counts_[ps].at((size_t)K * kNumDirs + kN);
+      a.need_inc[1] = (unsigned long long)pst_counts_[ps].at((size_t)K * 2 + 0);  // S's north pushes
       a.sig[1] = reinterpret_cast<unsigned long long*>(ipc_blocks_[ps] + sl.flag[kN]);
       for (int p = 0; p < 2; ++p) {
         a.hsrc[1][p] = reinterpret_cast<const float*>(ipc_block_ + me.recv_s[p] - (g.G + g.xcell) * rowb);
@@ -1506,10 +1507,19 @@ void Engine::launch_pstream_chunks(int K, int J) {
     a.rel = opt_.direct_release < 0 ? 2 : opt_.direct_release;
     a.acq = opt_.direct_acquire < 0 ? 1 : opt_.direct_acquire;
   }
-  launch_pstream(a, K, opt_.precision, compute_);
+  launch_pstream(a, K, opt_.precision, P.cpl, compute_);
   P.cdone += (unsigned)J;
   ++pstream_launches_;
   progress_tick(compute_);
+}
+
+bool Engine::pst_everywhere(int K) const {
+  // single process without exchange: only this engine's plan matters
+  if (!direct_) return true;
+  if (pst_counts_.empty()) return false;
+  for (const auto& v : pst_counts_)
+    if ((size_t)K * 2 >= v.size() || v[(size_t)K * 2] < 0) return false;
+  return true;
 }
 
 std::vector<PUnit> Engine::pstream_units(int K) {
@@ -1880,8 +1890,18 @@ std::string Engine::ipc_handle() {
       const UnitLists& U = units(0, K);
       for (int d = 0; d < kNumDirs; ++d) counts[(size_t)K * kNumDirs + d] = U.pushes[d];
     }
+  // ... and its persistent plan's N / S halo pushes per chunk at each depth (-1: no plan)
+  std::vector<int32_t> pcounts((size_t)(G_ + 1) * 2, -1);
+  for (int K = 1; K <= G_; ++K) {
+    const PPlan* P = pplan(K);
+    if (P != nullptr) {
+      pcounts[(size_t)K * 2] = P->pushes[0];
+      pcounts[(size_t)K * 2 + 1] = P->pushes[1];
+    }
+  }
   std::string blob(reinterpret_cast<const char*>(&h), sizeof(h));
   blob.append(reinterpret_cast<const char*>(counts.data()), counts.size() * sizeof(int32_t));
+  blob.append(reinterpret_cast<const char*>(pcounts.data()), pcounts.size() * sizeof(int32_t));
   return blob;
 }
 
@@ -1890,16 +1910,20 @@ void Engine::ipc_open(const std::vector<std::string>& handles) {
   const int me = tiles_.at(0).rank, nr = dec_.nranks();
   if ((int)handles.size() != nr) throw std::invalid_argument("ipc_open: one handle per rank expected");
   if (nr > kIpcMaxRanks) throw std::invalid_argument("ipc_open: too many ranks");
-  const size_t want = sizeof(hipIpcMemHandle_t) + (size_t)(G_ + 1) * kNumDirs * sizeof(int32_t);
+  const size_t nc = (size_t)(G_ + 1) * kNumDirs, npc = (size_t)(G_ + 1) * 2;
+  const size_t want = sizeof(hipIpcMemHandle_t) + (nc + npc) * sizeof(int32_t);
   H2D_HIP_CHECK(hipSetDevice(opt_.device));
   ipc_blocks_.assign(nr, nullptr);
   ipc_opened_.assign(nr, false);
   ipc_counts_.assign(nr, std::vector<int32_t>());
+  pst_counts_.assign(nr, std::vector<int32_t>());
   for (int r = 0; r < nr; ++r) {
     if (handles[r].size() != want) throw std::invalid_argument("ipc_open: bad handle (another build or halo depth?)");
-    ipc_counts_[r].resize((size_t)(G_ + 1) * kNumDirs);
-    std::memcpy(ipc_counts_[r].data(), handles[r].data() + sizeof(hipIpcMemHandle_t),
-                ipc_counts_[r].size() * sizeof(int32_t));
+    ipc_counts_[r].resize(nc);
+    std::memcpy(ipc_counts_[r].data(), handles[r].data() + sizeof(hipIpcMemHandle_t), nc * sizeof(int32_t));
+    pst_counts_[r].resize(npc);
+    std::memcpy(pst_counts_[r].data(), handles[r].data() + sizeof(hipIpcMemHandle_t) + nc * sizeof(int32_t),
+                npc * sizeof(int32_t));
     if (r == me) {
       ipc_blocks_[r] = ipc_block_;
       continue;

@@ -93,6 +93,9 @@ struct EngineOptions {
   // launch on an aligned unit grid (single tile without exchange, or the direct IPC pipeline of
   // row strips).  -1 auto, 0 off, 1 on.
   int persistent = -1;
+  // Strip width of the persistent kernel: 256 (4 columns per lane), 128 (2 per lane: units twice
+  // as tall for the same wave count, so a short tile's K-cone costs half as much), 0 auto.
+  int pstream_cols = 0;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
   // Diagnostics: record the per-wave timeline (s_memrealtime stamps) of the first `timeline`
@@ -363,9 +366,15 @@ class Engine {
     PUnit* d_units = nullptr;
     unsigned* d_prog = nullptr;  // progress words, 32 apart
     int n = 0;
+    int cpl = 4;                 // columns per lane (strip width 64 * cpl)
+    int pushes[2] = {0, 0};      // N / S halo units (direct pipeline): flag increments per chunk
     unsigned cdone = 0;          // chunks run by this plan's launches (progress base)
     std::vector<PUnit> host;
   };
+  // per rank, per (K, N/S): its persistent plan's halo pushes per chunk (-1: no plan at depth K),
+  // from the IPC handles; a depth runs persistent launches only if every rank has a plan
+  std::vector<std::vector<int32_t>> pst_counts_;
+  bool pst_everywhere(int K) const;
   std::map<int, PPlan> pplans_;  // by K (an empty plan: not eligible)
   int64_t pstream_launches_ = 0;
   const PPlan* pplan(int K);     // build / look up; nullptr if depth K runs launch per chunk

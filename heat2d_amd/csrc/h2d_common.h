@@ -110,6 +110,10 @@ struct TileGeom {
 constexpr int kWaveCols = 256;
 inline int64_t lead_cols(int K) { return (int64_t)((K + 3) & ~3); }
 inline int64_t strip_out_cols(int K) { return kWaveCols - 2 * lead_cols(K); }
+// Narrow strips of the persistent kernel: `cpl` columns per lane (4: 256-column strips, 2:
+// 128-column strips), the lead R rounded to whole lanes.
+inline int64_t wave_cols(int cpl) { return 64 * (int64_t)cpl; }
+inline int64_t lead_cols(int K, int cpl) { return (int64_t)((K + cpl - 1) / cpl * cpl); }
 
 // Directions of the 8-neighbour halo exchange (x = row index, y = column index).
 enum Dir : int { kN = 0, kS, kW, kE, kNW, kNE, kSW, kSE, kNumDirs };

@@ -51,14 +51,16 @@ constexpr int kSideLinks = 6;
 // columns of one ghost-column group of the 2-D direct receive buffer (>= the deepest lead R)
 constexpr int kGhostGroup = 16;
 
-int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t cb, bool fixed, bool per_x, bool per_y);
+int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t cb, bool fixed, bool per_x, bool per_y,
+                    int64_t wcols = kWaveCols);
 // Column strips of a tile for depth K.  Interior strips output 256 - 2R columns; with fixed
 // edges a strip at a global edge column is edge-aligned and outputs 256 - R (4096 columns at
 // K=8: 248 + 15×240 + 248 = 17 strips instead of 18).
 struct Strip {
   int64_t cb, lo, hi;
 };
-std::vector<Strip> strip_layout(const TileGeom& g, int K, bool fixed, bool per_y);
+// cpl: columns per lane (4: 256-column strips; 2: the persistent kernel's 128-column strips).
+std::vector<Strip> strip_layout(const TileGeom& g, int K, bool fixed, bool per_y, int cpl = 4);
 // Cut a tile into work units for depth K: ~H rows per unit, edge units shortened by
 // `edge_weight` so that every wave finishes at about the same time (one wave round).
 // H > 0 fixes the rows of a plain unit; H == 0 sizes units to fill `capacity` resident waves.
@@ -221,14 +223,16 @@ struct PStreamArgs {
 };
 // Largest K with a compiled persistent kernel (K <= 8, write-through stores).
 constexpr int kMaxPK = 8;
-void launch_pstream(const PStreamArgs& a, int K, int precision, hipStream_t s);
+// cpl: columns per lane of the plan (4 or 2), a template parameter of the kernel.
+void launch_pstream(const PStreamArgs& a, int K, int precision, int cpl, hipStream_t s);
 // Resident 256-thread blocks per CU of the persistent kernel (every block must be resident).
-int pstream_blocks_per_cu(int K, int precision);
+int pstream_blocks_per_cu(int K, int precision, int cpl);
 void warm_pstream_kernels(int precision, int kmax, hipStream_t s);
 // The aligned unit grid of the persistent kernel (empty if the tile does not allow one):
-// `bands` row bands (even when both halo directions exist), every band at least hmin rows.
+// `bands` row bands (even when both halo directions exist), every band at least hmin rows;
+// strips of 64 * cpl columns.
 std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x, bool per_y, double row_edge_weight,
-                                int64_t capacity, bool halo_n, bool halo_s, int hmin);
+                                int64_t capacity, bool halo_n, bool halo_s, int hmin, int cpl = 4);
 
 // Largest K with a compiled streaming kernel.
 constexpr int kMaxK = 16;
@@ -279,8 +283,8 @@ template <int K, bool F32, bool RESID>
 void launch_stream_kv(const StreamArgs& a, hipStream_t s);
 template <int K, bool F32, bool RESID>
 int stream_blocks_per_cu_v();
-template <int K, bool F32>
+template <int K, bool F32, int CPL>
 void launch_pstream_kv(const PStreamArgs& a, hipStream_t s);
-template <int K, bool F32>
+template <int K, bool F32, int CPL>
 int pstream_blocks_per_cu_v();
 }  // namespace h2d

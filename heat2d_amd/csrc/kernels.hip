@@ -323,19 +323,19 @@ int64_t stream_wave_capacity(int K, int precision, int device) {
   return (int64_t)bpc * cus * 4;
 }
 
-std::vector<Strip> strip_layout(const TileGeom& g, int K, bool fixed, bool per_y) {
-  const int64_t R = lead_cols(K), wout = strip_out_cols(K);
-  const bool wide = fixed && !per_y && g.ycell >= kWaveCols;
+std::vector<Strip> strip_layout(const TileGeom& g, int K, bool fixed, bool per_y, int cpl) {
+  const int64_t W = wave_cols(cpl), R = lead_cols(K, cpl), wout = W - 2 * R;
+  const bool wide = fixed && !per_y && g.ycell >= W;
   const bool lo_edge = wide && g.gy0 == 0;
   const bool hi_edge = wide && g.gy0 + g.ycell == g.NY;
   std::vector<Strip> v;
   int64_t a = 0, b = g.ycell, rcb = 0;
   if (lo_edge) {
-    v.push_back(Strip{0, 0, kWaveCols - R});
-    a = kWaveCols - R;
+    v.push_back(Strip{0, 0, W - R});
+    a = W - R;
   }
   if (hi_edge) {
-    rcb = ((g.ycell + 3) & ~int64_t(3)) - kWaveCols;  // window ends at the (4-aligned) edge
+    rcb = (g.ycell + cpl - 1) / cpl * cpl - W;  // window ends at the (lane-aligned) edge
     b = std::max(a, rcb + R);
   }
   for (int64_t p = a; p < b; p += wout) v.push_back(Strip{p - R, p, std::min(p + wout, b)});
@@ -343,10 +343,11 @@ std::vector<Strip> strip_layout(const TileGeom& g, int K, bool fixed, bool per_y
   return v;
 }
 
-int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t cb, bool fixed, bool per_x, bool per_y) {
+int unit_edge_flags(const TileGeom& g, int K, int64_t x0, int64_t h, int64_t cb, bool fixed, bool per_x, bool per_y,
+                    int64_t wcols) {
   int f = 0;
   if (!per_y) {
-    const int64_t lo = g.gy0 + cb, hi = lo + kWaveCols - 1;  // the wave's column window
+    const int64_t lo = g.gy0 + cb, hi = lo + wcols - 1;  // the wave's column window
     const bool sp = fixed ? ((lo <= 0 && 0 <= hi) || (lo <= g.NY - 1 && g.NY - 1 <= hi)) : (lo < 0 || hi >= g.NY);
     if (sp) f |= kEdgeCols;
   }
@@ -511,19 +512,27 @@ void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hip
 
 // ---- persistent pipelined variant (pstream_kernel.hpp, generated TUs pstream_k<K>_f<F>.hip) ----
 #define H2D_PK_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
-#define H2D_PEXTERN(K)                                                              \
-  extern template void launch_pstream_kv<K, false>(const PStreamArgs&, hipStream_t); \
-  extern template void launch_pstream_kv<K, true>(const PStreamArgs&, hipStream_t);  \
-  extern template int pstream_blocks_per_cu_v<K, false>();                           \
-  extern template int pstream_blocks_per_cu_v<K, true>();
+#define H2D_PEXTERN(K)                                                                 \
+  extern template void launch_pstream_kv<K, false, 4>(const PStreamArgs&, hipStream_t); \
+  extern template void launch_pstream_kv<K, true, 4>(const PStreamArgs&, hipStream_t);  \
+  extern template void launch_pstream_kv<K, false, 2>(const PStreamArgs&, hipStream_t); \
+  extern template void launch_pstream_kv<K, true, 2>(const PStreamArgs&, hipStream_t);  \
+  extern template int pstream_blocks_per_cu_v<K, false, 4>();                           \
+  extern template int pstream_blocks_per_cu_v<K, true, 4>();                            \
+  extern template int pstream_blocks_per_cu_v<K, false, 2>();                           \
+  extern template int pstream_blocks_per_cu_v<K, true, 2>();
 H2D_PK_LIST(H2D_PEXTERN)
 #undef H2D_PEXTERN
 
-void launch_pstream(const PStreamArgs& a, int K, int precision, hipStream_t s) {
+void launch_pstream(const PStreamArgs& a, int K, int precision, int cpl, hipStream_t s) {
   const bool f32 = precision == kFp32;
+  if (cpl != 2 && cpl != 4) throw std::invalid_argument("persistent stencil: 2 or 4 columns per lane");
   switch (K) {
-#define H2D_CASE(KK) \
-  case KK: f32 ? launch_pstream_kv<KK, true>(a, s) : launch_pstream_kv<KK, false>(a, s); break;
+#define H2D_CASE(KK)                                                                             \
+  case KK:                                                                                       \
+    if (cpl == 4) f32 ? launch_pstream_kv<KK, true, 4>(a, s) : launch_pstream_kv<KK, false, 4>(a, s); \
+    else f32 ? launch_pstream_kv<KK, true, 2>(a, s) : launch_pstream_kv<KK, false, 2>(a, s);          \
+    break;
     H2D_PK_LIST(H2D_CASE)
 #undef H2D_CASE
     default: throw std::invalid_argument("no persistent stencil compiled for K=" + std::to_string(K));
@@ -531,11 +540,13 @@ void launch_pstream(const PStreamArgs& a, int K, int precision, hipStream_t s) {
   H2D_HIP_CHECK(hipGetLastError());
 }
 
-int pstream_blocks_per_cu(int K, int precision) {
+int pstream_blocks_per_cu(int K, int precision, int cpl) {
   const bool f32 = precision == kFp32;
   switch (K) {
-#define H2D_CASE(KK) \
-  case KK: return f32 ? pstream_blocks_per_cu_v<KK, true>() : pstream_blocks_per_cu_v<KK, false>();
+#define H2D_CASE(KK)                                                                                 \
+  case KK:                                                                                           \
+    if (cpl == 2) return f32 ? pstream_blocks_per_cu_v<KK, true, 2>() : pstream_blocks_per_cu_v<KK, false, 2>(); \
+    return f32 ? pstream_blocks_per_cu_v<KK, true, 4>() : pstream_blocks_per_cu_v<KK, false, 4>();
     H2D_PK_LIST(H2D_CASE)
 #undef H2D_CASE
     default: return 0;
@@ -545,13 +556,15 @@ int pstream_blocks_per_cu(int K, int precision) {
 void warm_pstream_kernels(int precision, int kmax, hipStream_t s) {
   PStreamArgs a{};
   a.nunits = 0;
-  for (int K = 1; K <= std::min(kmax, kMaxPK); ++K) launch_pstream(a, K, precision, s);
+  for (int K = 1; K <= std::min(kmax, kMaxPK); ++K)
+    for (int cpl : {4, 2}) launch_pstream(a, K, precision, cpl, s);
 }
 
 std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x, bool per_y, double row_edge_weight,
-                                int64_t capacity, bool halo_n, bool halo_s, int hmin) {
+                                int64_t capacity, bool halo_n, bool halo_s, int hmin, int cpl) {
   std::vector<PUnit> out;
-  const std::vector<Strip> strips = strip_layout(g, K, fixed, per_y);
+  const int64_t W = wave_cols(cpl);
+  const std::vector<Strip> strips = strip_layout(g, K, fixed, per_y, cpl);
   const int S = (int)strips.size();
   if (S < 1 || capacity < S) return out;
   hmin = std::max(hmin, K);  // a K-cone spans at most the adjacent bands
@@ -567,7 +580,7 @@ std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x
   for (;;) {
     std::vector<double> w(m, 1.0);
     auto row_edge = [&](int64_t lo, int64_t hi) {  // rows [lo, hi) of the tile, cone K
-      return (unit_edge_flags(g, K, lo, hi - lo, strips[S / 2].cb, fixed, per_x, true) & kEdgeRows) != 0;
+      return (unit_edge_flags(g, K, lo, hi - lo, strips[S / 2].cb, fixed, per_x, true, W) & kEdgeRows) != 0;
     };
     // first estimate with equal bands, then the weights of the bands at the tile's edge rows
     const int64_t eq = g.xcell / m;
@@ -598,7 +611,7 @@ std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x
     for (int s = 0; s < S; ++s) {
       PUnit& p = out[(size_t)uidx(i, s)];
       const Strip& st = strips[(size_t)s];
-      p.u = Unit{s, (int)a0[i], (int)hh[i], unit_edge_flags(g, K, a0[i], hh[i], st.cb, fixed, per_x, per_y),
+      p.u = Unit{s, (int)a0[i], (int)hh[i], unit_edge_flags(g, K, a0[i], hh[i], st.cb, fixed, per_x, per_y, W),
                  (int)st.cb, (int)st.lo, (int)st.hi, 0};
       if (i & 1) p.u.flags |= kUnitReverse;
       if ((i == 0 && halo_n) || (i == m - 1 && halo_s)) p.u.flags |= kUnitNS;
@@ -614,7 +627,7 @@ std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x
       PUnit& p = out[(size_t)uidx(i, s)];
       const int64_t x0 = a0[i], h = hh[i];
       const bool rev = (i & 1) != 0;
-      const int64_t wlo = strips[(size_t)s].cb, whi = wlo + kWaveCols;  // my column window
+      const int64_t wlo = strips[(size_t)s].cb, whi = wlo + W;  // my column window
       // a window must not reach past the adjacent strips' outputs
       for (int s2 = 0; s2 < S; ++s2)
         if (std::abs(s2 - s) > 1 && strips[(size_t)s2].lo < whi && strips[(size_t)s2].hi > wlo) return {};

@@ -35,11 +35,31 @@
 namespace h2d {
 namespace {
 
-// sc1 (L1-bypassing, coherent for write-through hand-offs) 16-byte row load of one lane.
-__device__ __forceinline__ float4 load_row_sc1(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+// sc1 (L1-bypassing, coherent for write-through hand-offs) row load of one lane: 16 bytes
+// (4 columns per lane, 256-column strips) or 8 bytes (2 columns, 128-column strips).
+template <class V>
+__device__ __forceinline__ V load_row_sc1(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff);
+template <>
+__device__ __forceinline__ float4 load_row_sc1<float4>(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
   const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 16 /* sc1 */);
   return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
 }
+template <>
+__device__ __forceinline__ float2 load_row_sc1<float2>(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  const u32x2 d = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, soff, 16 /* sc1 */);
+  return make_float2(__uint_as_float(d.x), __uint_as_float(d.y));
+}
+
+template <int CPL>
+struct LaneVec;
+template <>
+struct LaneVec<4> {
+  typedef float4 T;
+};
+template <>
+struct LaneVec<2> {
+  typedef float2 T;
+};
 
 // Lane l < kPSlots holds neighbour slot l; other lanes are inert (nb < 0).
 struct PSlot {
@@ -90,14 +110,15 @@ __device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int la
   if (lane == 0) __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <int K, bool F32, int EDGE, bool FIXED>
+template <int K, bool F32, int EDGE, bool FIXED, int CPL>
 __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w, int lane, PSlot& sl) {
+  typedef typename LaneVec<CPL>::T V;
   const int h = u.h, n = h + 2 * K;
   const bool rev = (u.flags & kUnitReverse) != 0;
   const bool ns = (u.flags & kUnitNS) != 0;
   const int dir = rev ? 1 : 0;
   const int64_t x0 = u.x0;
-  const int64_t cb = (int64_t)u.cb + 4 * lane;
+  const int64_t cb = (int64_t)u.cb + CPL * lane;
   const int64_t xin = rev ? x0 + h - 1 + K : x0 - K;
   const int64_t xout = rev ? x0 + h - 1 : x0;
   const int pb = (int)(a.pitch * (int64_t)sizeof(float));  // row bytes (the host keeps n * pb < 2^31)
@@ -113,16 +134,16 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   auto colmask = [&](int64_t q) { return a.fixed ? (q == 0 || q == a.NY - 1) : (q < 0 || q >= a.NY); };
   c.m0 = colmask(gc + 0);
   c.m1 = colmask(gc + 1);
-  c.m2 = colmask(gc + 2);
-  c.m3 = colmask(gc + 3);
+  c.m2 = CPL > 2 && colmask(gc + 2);
+  c.m3 = CPL > 2 && colmask(gc + 3);
   const bool in_out = (cb >= u.olo) && (cb < u.ohi);
-  c.sout = a.dummy + 4 * lane;  // unused: write-through path
+  c.sout = a.dummy + CPL * lane;  // unused: write-through path
   c.spitch = 0;
   c.obs = rev ? -pb : pb;
   c.obo = rev ? (h - 1) * pb : 0;
-  c.voff = in_out ? 16u * (unsigned)lane : 0x80000000u;
+  c.voff = in_out ? 4u * CPL * (unsigned)lane : 0x80000000u;
   c.st0 = c.st1 = c.st2 = c.st3 = false;
-  c.kout = a.dummy + 4 * lane;
+  c.kout = a.dummy + CPL * lane;
   c.kpitch = 0;
   c.rel = a.rel;
   c.spu = false;
@@ -138,8 +159,8 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   const int64_t in_base = (a.G + x0 - K) * a.pitch + a.PL + u.cb;  // lowest input row, lane 0
   const int64_t out_base = (a.G + x0) * a.pitch + a.PL + u.cb;     // lowest output row, lane 0
   const int64_t lane_in = (a.G + xin) * a.pitch + a.PL + cb;       // first stream row, this lane
-  const int64_t pitch4 = rev ? -(a.pitch >> 2) : (a.pitch >> 2);
-  const unsigned lvoff = 16u * (unsigned)lane;
+  const int64_t pitchv = rev ? -(a.pitch / CPL) : (a.pitch / CPL);  // a row, in lane vectors
+  const unsigned lvoff = 4u * CPL * (unsigned)lane;
   auto soff = [&](int r) { return rev ? (n - 1 - r) * pb : r * pb; };
 
   bool dead = false;         // a wait gave up: finish without waiting (the host reports it)
@@ -164,7 +185,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       sl.known = max(sl.known, pv);
       pensure(sl, 0, min(n, 2 * K + 4), cidx - 1u, a.prog, a, dead);
     }
-    const float4* hrowp = nullptr;
+    const V* hrowp = nullptr;
     if (ns && a.wait[dir] != nullptr) {
       // the neighbour GPU's pushes of its chunk j-1 (this chunk's ghost rows)
       if (lane == 0 && !dead && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
@@ -188,27 +209,27 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       if (a.acq == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       else if (a.acq == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      hrowp = reinterpret_cast<const float4*>(a.hsrc[dir][ipar] + lane_in);
+      hrowp = reinterpret_cast<const V*>(a.hsrc[dir][ipar] + lane_in);
     }
     c.obase = dst + out_base;
-    c.pout = (pushes && in_out) ? a.push[dir][ipar ^ 1] + xout * a.pitch + a.PL + cb : a.dummy + 4 * lane;
+    c.pout = (pushes && in_out) ? a.push[dir][ipar ^ 1] + xout * a.pitch + a.PL + cb : a.dummy + CPL * lane;
     c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
     const __amdgpu_buffer_rsrc_t rin =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src) + in_base, (short)0, n * pb, 0x00020000);
 
-    float4 S[K][2];
+    V S[K][2];
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-      S[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
-      S[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      S[t][0] = V{};
+      S[t][1] = V{};
     }
-    float4 pro[2 * K];
+    V pro[2 * K];
 #pragma unroll
-    for (int i = 0; i < 2 * K; ++i) pro[i] = (i < K && hrowp != nullptr) ? hrowp[(int64_t)i * pitch4]
-                                                                        : load_row_sc1(rin, lvoff, soff(i));
-    float4 pf[4];
+    for (int i = 0; i < 2 * K; ++i) pro[i] = (i < K && hrowp != nullptr) ? hrowp[(int64_t)i * pitchv]
+                                                                        : load_row_sc1<V>(rin, lvoff, soff(i));
+    V pf[4];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) pf[d] = load_row_sc1(rin, lvoff, soff(min(2 * K + d, n - 1)));
+    for (int d = 0; d < 4; ++d) pf[d] = load_row_sc1<V>(rin, lvoff, soff(min(2 * K + d, n - 1)));
     __builtin_amdgcn_sched_barrier(0);
     prologue<K, F32, EDGE, FIXED, false, true, false, 0>(S, pro, c, k, racc);
 
@@ -219,8 +240,8 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
     bool have_poll = false;
 #define H2D_PSTEADY(D)                                                                \
   {                                                                                   \
-    const float4 nw = pf[D];                                                          \
-    pf[D] = load_row_sc1(rin, lvoff, soff(min(ir0 + (D) + 4, n - 1)));                \
+    const V nw = pf[D];                                                               \
+    pf[D] = load_row_sc1<V>(rin, lvoff, soff(min(ir0 + (D) + 4, n - 1)));             \
     process_row<K, F32, EDGE, FIXED, false, true, false, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
     for (; ir0 + 4 <= n; ir0 += 4) {
@@ -254,7 +275,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   if (sig_pending) psignal(a.sig[dir], a.rel, lane);
 }
 
-template <int K, bool F32>
+template <int K, bool F32, int CPL>
 __global__ __launch_bounds__(256) void pstream_kernel(PStreamArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int w = (int)blockIdx.x * 4 + wv;
@@ -277,35 +298,35 @@ __global__ __launch_bounds__(256) void pstream_kernel(PStreamArgs a) {
   sl.known = 0u;
   const bool fixed = a.fixed != 0;
   switch (u.flags & 3) {
-    case 0: prun<K, F32, 0, false>(a, u, w, lane, sl); break;
+    case 0: prun<K, F32, 0, false, CPL>(a, u, w, lane, sl); break;
     case 1:
-      if (fixed) prun<K, F32, 1, true>(a, u, w, lane, sl);
-      else prun<K, F32, 1, false>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 1, true, CPL>(a, u, w, lane, sl);
+      else prun<K, F32, 1, false, CPL>(a, u, w, lane, sl);
       break;
     case 2:
-      if (fixed) prun<K, F32, 2, true>(a, u, w, lane, sl);
-      else prun<K, F32, 2, false>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 2, true, CPL>(a, u, w, lane, sl);
+      else prun<K, F32, 2, false, CPL>(a, u, w, lane, sl);
       break;
     default:
-      if (fixed) prun<K, F32, 3, true>(a, u, w, lane, sl);
-      else prun<K, F32, 3, false>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 3, true, CPL>(a, u, w, lane, sl);
+      else prun<K, F32, 3, false, CPL>(a, u, w, lane, sl);
       break;
   }
 }
 
 }  // namespace
 
-template <int K, bool F32>
+template <int K, bool F32, int CPL>
 void launch_pstream_kv(const PStreamArgs& a, hipStream_t s) {
   const int blocks = std::max(1, (a.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_pstream_kernels)
-  hipLaunchKernelGGL((pstream_kernel<K, F32>), dim3(blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((pstream_kernel<K, F32, CPL>), dim3(blocks), dim3(256), 0, s, a);
 }
 
-template <int K, bool F32>
+template <int K, bool F32, int CPL>
 int pstream_blocks_per_cu_v() {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(pstream_kernel<K, F32>), 256,
-                                                   0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(pstream_kernel<K, F32, CPL>),
+                                                   256, 0) != hipSuccess)
     return 0;
   return nb;
 }

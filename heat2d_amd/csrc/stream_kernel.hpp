@@ -105,6 +105,28 @@ __device__ __forceinline__ float4 row_update(const float4& P, const float4& C, c
   return o;
 }
 
+// The same row update for a lane that owns 2 columns (128-column strips of the persistent
+// kernel): lane i holds (x, y) = columns (2i, 2i+1); west of x is the left lane's y, east of y
+// is the right lane's x.
+template <bool F32>
+__device__ __forceinline__ float2 row_update(const float2& P, const float2& C, const float2& N, const Coef& k) {
+  const f32x2 sn = f32x2{P.x, P.y} + f32x2{N.x, N.y};
+  const float ew0 = from_left(C.y) + C.y;
+  const float ew1 = C.x + from_right(C.x);
+  float2 o;
+  if constexpr (F32) {
+    const f32x2 c01 = {C.x, C.y}, ew01 = {ew0, ew1};
+    const f32x2 m2 = {-2.0f, -2.0f}, cx2 = {k.cxf, k.cxf}, cy2 = {k.cyf, k.cyf};
+    f32x2 r = __builtin_elementwise_fma(cx2, __builtin_elementwise_fma(m2, c01, sn), c01);
+    r = __builtin_elementwise_fma(cy2, __builtin_elementwise_fma(m2, c01, ew01), r);
+    o = make_float2(r.x, r.y);
+  } else {
+    o.x = cell<F32>(C.x, sn.x, ew0, k);
+    o.y = cell<F32>(C.y, sn.y, ew1, k);
+  }
+  return o;
+}
+
 struct LaneCtx {
   int64_t gxb;     // global row of stream input index 0
   int64_t dir;     // +1: rows stream top-down, -1: bottom-up (kUnitReverse)
@@ -165,6 +187,15 @@ __device__ __forceinline__ void store_row_wt(float* base, unsigned voff, int sof
   __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)voff, soff, 16 /* sc1 */);
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// The 2-column lane's row store (buffer_store_dwordx2 ... sc1).
+__device__ __forceinline__ void store_row_wt(float* base, unsigned voff, int soff, const float2& o) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  const u32x2 d = {__float_as_uint(o.x), __float_as_uint(o.y)};
+  __builtin_amdgcn_raw_buffer_store_b64(d, r, (int)voff, soff, 16 /* sc1 */);
+}
+
 __device__ __forceinline__ double sq_diff(float a, float b) {
   const double d = (double)a - (double)b;
   return d * d;
@@ -208,11 +239,38 @@ __device__ __forceinline__ float4 apply_edge(float4 o, const float4& C, int64_t 
   return o;
 }
 
+template <int EDGE, bool FIXED>
+__device__ __forceinline__ float2 apply_edge(float2 o, const float2& C, int64_t gr, const LaneCtx& c) {
+  if constexpr ((EDGE & 1) != 0) {
+    if constexpr (FIXED) {
+      o.x = c.m0 ? C.x : o.x;
+      o.y = c.m1 ? C.y : o.y;
+    } else {
+      o.x = c.m0 ? 0.0f : o.x;
+      o.y = c.m1 ? 0.0f : o.y;
+    }
+  }
+  if constexpr ((EDGE & 2) != 0) {
+    if constexpr (FIXED) {
+      const bool r = gr == 0 || gr == c.NX - 1;
+      o.x = r ? C.x : o.x;
+      o.y = r ? C.y : o.y;
+    } else {
+      const bool r = gr < 0 || gr >= c.NX;
+      o.x = r ? 0.0f : o.x;
+      o.y = r ? 0.0f : o.y;
+    }
+  }
+  return o;
+}
+
 // Process stream input row `ir` (level-0 value `cur`) through levels 1..TMAX (TMAX <= K).
 // Slot parity P = ir & 1: S[l][P] holds level-l row (ir-l-2), S[l][1-P] holds row (ir-l-1).
 // Level t computes row (ir - t) of level t.  Level K writes output row ir - 2K (unit-relative).
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int P, int TMAX>
-__device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int ir, const LaneCtx& c, const Coef& k,
+// V: the lane's cells of a row (float4: 256-column strips; float2: 128-column strips, no
+// residual / side pushes).
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int P, int TMAX, class V>
+__device__ __forceinline__ void process_row(V (&S)[K][2], V cur, int ir, const LaneCtx& c, const Coef& k,
                                             double& racc) {
 #pragma unroll
   for (int t = 1; t <= K; ++t) {
@@ -220,16 +278,16 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
       if (t - 1 <= TMAX) S[t - 1][P] = cur;  // save the last active level's new row
       continue;
     }
-    const float4 prv = S[t - 1][P];
-    const float4 mid = S[t - 1][1 - P];
-    float4 o = row_update<F32>(prv, mid, cur, k);
+    const V prv = S[t - 1][P];
+    const V mid = S[t - 1][1 - P];
+    V o = row_update<F32>(prv, mid, cur, k);
     if constexpr (EDGE != 0) o = apply_edge<EDGE, FIXED>(o, mid, c.gxb + c.dir * (ir - t), c);
     S[t - 1][P] = cur;
     if (t == K) {
       const int64_t orow = ir - 2 * K;
       if constexpr (WT) store_row_wt(c.obase, c.voff, c.obo + (int)orow * c.obs, o);
-      else *reinterpret_cast<float4*>(c.sout + orow * c.spitch) = o;
-      if (orow < c.prows) *reinterpret_cast<float4*>(c.pout + orow * c.ppitch) = o;  // uniform branch
+      else *reinterpret_cast<V*>(c.sout + orow * c.spitch) = o;
+      if (orow < c.prows) *reinterpret_cast<V*>(c.pout + orow * c.ppitch) = o;  // uniform branch
       if constexpr (SIDE) side_push(o, orow, c);
       if constexpr (RESID) {
         *reinterpret_cast<float4*>(c.kout + orow * c.kpitch) = mid;
@@ -244,9 +302,9 @@ __device__ __forceinline__ void process_row(float4 (&S)[K][2], float4 cur, int i
 }
 
 // Prologue row IR (compile-time): levels t <= IR/2 are primed, from rows already in registers.
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int IR>
-__device__ __forceinline__ void prologue(float4 (&S)[K][2], const float4 (&pro)[2 * K], const LaneCtx& c,
-                                         const Coef& k, double& racc) {
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int IR, class V>
+__device__ __forceinline__ void prologue(V (&S)[K][2], const V (&pro)[2 * K], const LaneCtx& c, const Coef& k,
+                                         double& racc) {
   if constexpr (IR < 2 * K) {
     process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR & 1, IR / 2>(S, pro[IR], IR, c, k, racc);
     prologue<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR + 1>(S, pro, c, k, racc);

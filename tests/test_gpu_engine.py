@@ -445,7 +445,29 @@ def test_fused_convergence_matches_oracle(native, gpu, gx, gy, pipeline):
         eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
                             small_grid_lds=False, tiled=0, **PIPELINES[pipeline], **CONV)
         st = eng.run(3000)
-        assert st["converged"] and st["steps_done"] == ref["steps_done"], (fused, st)
+        if not (st["converged"] and st["steps_done"] == ref["steps_done"]):
+            # diagnose: is the grid wrong, or only the residual?
+            plain = oracle(native, nx, ny, int(st["steps_done"]), 1)["grid"]
+            got = _gather(eng, nx, ny)
+            bad = got != plain
+            r, c = np.nonzero(bad)
+            # a fresh engine of the same configuration, 9 steps at a time: where does it first go wrong?
+            e2 = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
+                               small_grid_lds=False, tiled=0, **PIPELINES[pipeline],
+                               **{**CONV, "sensitivity": 0.0})
+            first = None
+            for i in range(1, 12):
+                e2.run(9)
+                b2 = _gather(e2, nx, ny) != oracle(native, nx, ny, 9 * i, 1)["grid"]
+                if b2.any():
+                    r2, c2 = np.nonzero(b2)
+                    first = (9 * i, int(b2.sum()), int(r2.min()), int(r2.max()), int(c2.min()), int(c2.max()))
+                    break
+            print(f"rerun: first wrong (steps, cells, rows, cols) {first}", flush=True)
+            pytest.fail(f"fused={fused}: converged {st['converged']} steps {st['steps_done']} residual "
+                        f"{st['residual']!r} (oracle {ref['residual']!r}); grid cells != oracle: {int(bad.sum())}"
+                        + (f" rows {r.min()}-{r.max()} cols {c.min()}-{c.max()} nan {int(np.isnan(got).sum())}"
+                           if bad.any() else "") + f"; path {st['path']} chunks {st['chunks']}")
         assert abs(st["residual"] - ref["residual"]) <= 1e-9 * ref["residual"]
         assert np.array_equal(_gather(eng, nx, ny), ref["grid"]), (gx, gy, pipeline, fused)
         # continuing re-checks at step 99 against the converged state: converged again, same state

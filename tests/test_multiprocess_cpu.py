@@ -129,7 +129,8 @@ def test_bench_contract_cpu_rehearsal(tmp_path, n):
     assert d["config"]["grid"] == [48, 48] and d["config"]["grid_per_gpu"] == [48 // n, 48]
     assert d["metric"] == "cell-updates/sec (whole node) + speedup/efficiency, 48^2 grid 6 steps"
     assert d["config"]["parallelism"] == ("single" if n == 1 else f"rows{n}")
-    assert d["config"]["tblock"] == 6  # short per-rank tiles (<= 1024 rows): depth 6 by default
+    # short per-rank tiles (<= 1024 rows) at N > 1: depth 8 (the persistent kernel's best), else 7
+    assert d["config"]["tblock"] == (8 if n > 1 else 7)
     assert abs(d["value"] - 48 * 48 * 6 / d["elapsed_s"]) / d["value"] < 1e-9
     assert abs(d["efficiency"] - d["speedup"] / n) < 1e-12
     if n > 1:

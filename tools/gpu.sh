@@ -27,7 +27,9 @@ for s in "$@"; do
     tests-nox) step tests-nox 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
     diagconv2) step diagconv2 300 python -u tools/diag_conv2.py ;;
     diagconv2b) HIP_LAUNCH_BLOCKING=1 step diagconv2b 300 python -u tools/diag_conv2.py ;;
+    diagstale) step diagstale 300 python -u tools/diag_stale.py ;;
     diagconv) step diagconv 300 python -u tools/diag_conv.py ;;
+    engine-file) step engine-file 600 python -u -m pytest tests/test_gpu_engine.py -q --timeout 300 --timeout-method thread -rf ;;
     tests-k) step tests-k 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf -k "$TESTK" ;;
     tests-new) step tests-new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
                  tests/test_gpu_engine.py -k "bench_shape or rank_tiles or timeline" ;;
@@ -39,6 +41,7 @@ for s in "$@"; do
     pcheck) step pcheck 300 python -u tools/pstream_check.py check ;;
     ptime) step ptime 300 python -u tools/pstream_check.py time ;;
     convtable) step convtable 600 python -u tools/conv_table.py ;;
+    pcols) step pcols 400 python -u tools/pstream_check.py cols ;;
     pksweep) step pksweep 300 python -u tools/pstream_check.py ksweep ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;

@@ -33,28 +33,29 @@ if "check" in what:
                                                (2048, 4096, 7, 140, 0, False), (203, 611, 1, 5, 0, False),
                                                (203, 611, 2, 7, 0, False), (203, 611, 3, 9, 1, False),
                                                (64, 611, 1, 5, 0, False), (512, 611, 1, 5, 0, False)]:
-        e = engine(nx, ny, K, 1, direct=direct, boundary=boundary, poison=True)
-        units = e.pstream_units(K)
-        hs = sorted({u[2] for u in units})
-        print(f"  plan: {len(units)} units, h {hs[:3]}..{hs[-3:]}" if units else "  plan: none", flush=True)
-        try:
-            st = e.run(steps)
-        except RuntimeError as ex:
-            print(f"check {nx}x{ny} K={K}: FAILED {ex}", flush=True)
-            continue
-        got = e.download(0)
-        ref = n.oracle_run(nx, ny, steps, boundary=boundary, periodic_x=direct)["grid"]
-        d = got != ref
-        r, c = np.nonzero(d)
-        print(f"check {nx}x{ny} K={K} steps={steps} b={boundary} direct={direct}: launches {e.pstream_launches()} "
-              f"chunks {st['chunks']} wrong {int(d.sum())}"
-              + (f" rows {r.min()}-{r.max()} cols {c.min()}-{c.max()} nan {int(np.isnan(got).sum())}" if d.any() else ""),
-              flush=True)
-        # continue: a second run (new launch, progress counters continue)
-        e.run(steps)
-        ref2 = n.oracle_run(nx, ny, 2 * steps, boundary=boundary, periodic_x=direct)["grid"]
-        print(f"   second run: wrong {int((e.download(0) != ref2).sum())}", flush=True)
-        del e
+      for cols in (256, 128):
+          e = engine(nx, ny, K, 1, direct=direct, boundary=boundary, poison=True, pstream_cols=cols)
+          units = e.pstream_units(K)
+          hs = sorted({u[2] for u in units})
+          print(f"  plan: {len(units)} units, h {hs[:3]}..{hs[-3:]}" if units else "  plan: none", flush=True)
+          try:
+              st = e.run(steps)
+          except RuntimeError as ex:
+              print(f"check {nx}x{ny} K={K}: FAILED {ex}", flush=True)
+              continue
+          got = e.download(0)
+          ref = n.oracle_run(nx, ny, steps, boundary=boundary, periodic_x=direct)["grid"]
+          d = got != ref
+          r, c = np.nonzero(d)
+          print(f"check {nx}x{ny} K={K} cols={cols} steps={steps} b={boundary} direct={direct}: launches {e.pstream_launches()} "
+                f"chunks {st['chunks']} wrong {int(d.sum())}"
+                + (f" rows {r.min()}-{r.max()} cols {c.min()}-{c.max()} nan {int(np.isnan(got).sum())}" if d.any() else ""),
+                flush=True)
+          # continue: a second run (new launch, progress counters continue)
+          e.run(steps)
+          ref2 = n.oracle_run(nx, ny, 2 * steps, boundary=boundary, periodic_x=direct)["grid"]
+          print(f"   second run: wrong {int((e.download(0) != ref2).sum())}", flush=True)
+          del e
 
 
 def timed(e, steps, reps=5):
@@ -91,4 +92,17 @@ if "ksweep" in what:
                 row.append(timed(e, 840))
                 del e
             print(f"ksweep {nx}x4096 K={K} direct: per-chunk {row[0]:.3f} us/step, persistent {row[1]:.3f} us/step",
+                  flush=True)
+
+
+if "cols" in what:
+    # strip width of the persistent kernel, direct row-periodic pipeline (per-rank strong-scaling tiles)
+    for nx in (512, 1024, 2048):
+        for K in (6, 7, 8):
+            row = []
+            for cols in (256, 128):
+                e = engine(nx, 4096, K, 1, direct=True, pstream_cols=cols)
+                row.append(timed(e, 840))
+                del e
+            print(f"cols {nx}x4096 K={K} direct persistent: 256-col {row[0]:.3f} us/step, 128-col {row[1]:.3f} us/step",
                   flush=True)
