@@ -173,6 +173,10 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     H2D_HIP_CHECK(hipHostMalloc(&h_resid_, sizeof(double) * (ranks.size() + 1)));
     d_lds_steps_ = dmalloc<long long>(1);
     d_dummy_ = dmalloc<float>(4 * kWaveCols);
+    if (o.phase_timers) {
+      d_phase_ = dmalloc<unsigned long long>(kPhases);
+      H2D_HIP_CHECK(hipMemset(d_phase_, 0, kPhases * sizeof(unsigned long long)));
+    }
     d_wait_acc_ = dmalloc<unsigned long long>(4);
     H2D_HIP_CHECK(hipMemset(d_wait_acc_, 0, 4 * sizeof(unsigned long long)));
     if (o.timeline > 0) {
@@ -376,6 +380,7 @@ Engine::~Engine() {
   hipFree(d_lds_steps_);
   hipFree(d_dummy_);
   hipFree(d_wait_acc_);
+  if (d_phase_) hipFree(d_phase_);
   if (d_stamps_) hipFree(d_stamps_);
   hipFree(d_send_);
   hipFree(d_recv_);
@@ -1476,6 +1481,7 @@ void Engine::launch_pstream_chunks(int K, int J) {
   a.timed_out = d_sig_timeout_;
   a.timed_out_host = h_timeout_dev_;
   a.wait_acc = d_wait_acc_;
+  a.phase = d_phase_;
   if (direct_) {
     const int64_t rowb = g.pitch * (int64_t)sizeof(float);
     const IpcLayout& me = ipc_lays_[T.rank];
@@ -1766,6 +1772,18 @@ void Engine::reset_halo_wait() {
   if (!on_gpu()) return;
   synchronize();
   H2D_HIP_CHECK(hipMemset(d_wait_acc_, 0, 4 * sizeof(unsigned long long)));
+  if (d_phase_) H2D_HIP_CHECK(hipMemset(d_phase_, 0, kPhases * sizeof(unsigned long long)));
+}
+
+std::vector<double> Engine::pstream_phases() const {
+  std::vector<double> out(kPhases, 0.0);
+  if (!on_gpu() || !d_phase_) return out;
+  synchronize();
+  unsigned long long v[kPhases];
+  H2D_HIP_CHECK(hipMemcpy(v, d_phase_, sizeof(v), hipMemcpyDeviceToHost));
+  out[0] = (double)v[0];
+  for (int i = 1; i < kPhases; ++i) out[i] = (double)v[i] * 0.01;  // s_memrealtime: 100 MHz
+  return out;
 }
 
 std::vector<Unit> Engine::unit_list(int t, int K, int which) {

@@ -96,6 +96,8 @@ struct EngineOptions {
   // Strip width of the persistent kernel: 256 (4 columns per lane), 128 (2 per lane: units twice
   // as tall for the same wave count, so a short tile's K-cone costs half as much), 0 auto.
   int pstream_cols = 0;
+  // Diagnostics: per-phase timers of the persistent kernel (PStreamArgs::phase)
+  bool phase_timers = false;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)
   bool trace = false;         // per-phase hipEvent timers + roctx ranges
   // Diagnostics: record the per-wave timeline (s_memrealtime stamps) of the first `timeline`
@@ -220,6 +222,8 @@ class Engine {
   };
   HaloWait halo_wait() const;
   void reset_halo_wait();
+  // persistent kernel phase timers (kPhases values: chunks, then microseconds summed over waves)
+  std::vector<double> pstream_phases() const;
   // Per-wave timeline of the launches recorded by the last run (EngineOptions::timeline):
   // {K, units, stamps[units][4] = start, ready (halo wait done), end, hardware id}.
   struct LaunchTimeline {
@@ -377,6 +381,7 @@ class Engine {
   bool pst_everywhere(int K) const;
   std::map<int, PPlan> pplans_;  // by K (an empty plan: not eligible)
   int64_t pstream_launches_ = 0;
+  unsigned long long* d_phase_ = nullptr;
   const PPlan* pplan(int K);     // build / look up; nullptr if depth K runs launch per chunk
   int plain_run(int64_t done, int64_t target, int k) const;  // equal plain chunks of depth k from `done`
   void launch_pstream_chunks(int K, int J);

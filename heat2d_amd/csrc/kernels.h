@@ -220,7 +220,13 @@ struct PStreamArgs {
   unsigned int* timed_out = nullptr;
   unsigned int* timed_out_host = nullptr;
   unsigned long long* wait_acc = nullptr;
+  // Diagnostics (usually null): s_memrealtime ticks (100 MHz) summed over waves and chunks, per
+  // phase of a chunk — [0] chunks, [1] chunk-start drain of the previous chunk's stores, [2]
+  // chunk-start wait for the neighbours' rows, [3] halo flag wait, [4] prologue (its loads and
+  // the cone rows), [5] steady rows + tail, [6] in-loop waits (the tops' vmcnt + row waits).
+  unsigned long long* phase = nullptr;
 };
+constexpr int kPhases = 7;
 // Largest K with a compiled persistent kernel (K <= 8, write-through stores).
 constexpr int kMaxPK = 8;
 // cpl: columns per lane of the plan (4 or 2), a template parameter of the kernel.

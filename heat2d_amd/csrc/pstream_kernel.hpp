@@ -166,6 +166,17 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   bool dead = false;         // a wait gave up: finish without waiting (the host reports it)
   bool sig_pending = false;  // a halo unit's pushes of its last chunk are not yet signalled
   double racc = 0.0;
+  // diagnostics: per-phase time of this wave (wave-uniform branch; no cost when a.phase is null)
+  const bool tm = a.phase != nullptr;
+  unsigned long long ph[kPhases] = {};
+  unsigned long long tq = tm ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  auto lap = [&](int i) {
+    if (tm) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      ph[i] += t - tq;
+      tq = t;
+    }
+  };
   for (int j = 0; j < a.nchunks; ++j) {
     const unsigned cidx = a.cbase + (unsigned)j;
     const int par = (a.cur0 + j) & 1;
@@ -175,6 +186,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
     if (j > 0) {
       // chunk start: my previous chunk's stores complete (the poll's wait drains them), publish
       // them, then the rows the up-front batch loads must be published by the neighbours
+      lap(5);
       const unsigned pv = ppoll(sl, a.prog);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       ppublish(myprog, cidx * (unsigned)h, lane);
@@ -183,7 +195,9 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
         sig_pending = false;
       }
       sl.known = max(sl.known, pv);
+      lap(1);
       pensure(sl, 0, min(n, 2 * K + 4), cidx - 1u, a.prog, a, dead);
+      lap(2);
     }
     const V* hrowp = nullptr;
     if (ns && a.wait[dir] != nullptr) {
@@ -210,6 +224,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       else if (a.acq == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       hrowp = reinterpret_cast<const V*>(a.hsrc[dir][ipar] + lane_in);
+      lap(3);
     }
     c.obase = dst + out_base;
     c.pout = (pushes && in_out) ? a.push[dir][ipar ^ 1] + xout * a.pitch + a.PL + cb : a.dummy + CPL * lane;
@@ -232,6 +247,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
     for (int d = 0; d < 4; ++d) pf[d] = load_row_sc1<V>(rin, lvoff, soff(min(2 * K + d, n - 1)));
     __builtin_amdgcn_sched_barrier(0);
     prologue<K, F32, EDGE, FIXED, false, true, false, 0>(S, pro, c, k, racc);
+    lap(4);
 
     int ir0 = 2 * K;
     int issued_prev = 0;  // output rows issued before the previous iteration top
@@ -246,6 +262,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   }
     for (; ir0 + 4 <= n; ir0 += 4) {
       // iteration top: every op before the previous top has completed (>= 8 VMEM ops since)
+      lap(5);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);
       if (pushes && !signalled && issued_prev >= a.sig_rows) {  // the pushed rows have completed
@@ -257,6 +274,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       have_poll = true;
       issued_prev = ir0 - 2 * K;
       if (j > 0) pensure(sl, ir0 + 4, min(n, ir0 + 8), cidx - 1u, a.prog, a, dead);
+      lap(6);
       H2D_PSTEADY(0)
       H2D_PSTEADY(1)
       H2D_PSTEADY(2)
@@ -270,9 +288,16 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
     // pushes not yet signalled at an iteration top: at the next chunk start (or launch end)
     if (pushes && !signalled) sig_pending = true;
   }
+  lap(5);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   ppublish(myprog, (a.cbase + (unsigned)a.nchunks) * (unsigned)h, lane);
   if (sig_pending) psignal(a.sig[dir], a.rel, lane);
+  lap(1);
+  if (tm && lane == 0) {
+    ph[0] = (unsigned long long)a.nchunks;
+#pragma unroll
+    for (int i = 0; i < kPhases; ++i) __hip_atomic_fetch_add(a.phase + i, ph[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <int K, bool F32, int CPL>

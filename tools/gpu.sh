@@ -42,6 +42,7 @@ for s in "$@"; do
     ptime) step ptime 300 python -u tools/pstream_check.py time ;;
     convtable) step convtable 600 python -u tools/conv_table.py ;;
     pcols) step pcols 400 python -u tools/pstream_check.py cols ;;
+    pphases) step pphases 300 python -u tools/pstream_check.py phases ;;
     pksweep) step pksweep 300 python -u tools/pstream_check.py ksweep ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;

@@ -106,3 +106,17 @@ if "cols" in what:
                 del e
             print(f"cols {nx}x4096 K={K} direct persistent: 256-col {row[0]:.3f} us/step, 128-col {row[1]:.3f} us/step",
                   flush=True)
+
+if "phases" in what:
+    # where a chunk's time goes (per wave, per chunk, us): phase timers of the persistent kernel
+    names = ["drain", "start-wait", "flag-wait", "prologue", "steady", "in-loop-wait"]
+    for nx, K, cols in ((512, 8, 128), (512, 8, 256), (1024, 8, 256), (1024, 8, 128), (4096, 7, 256)):
+        e = engine(nx, 4096, K, 1, direct=True, pstream_cols=cols, phase_timers=True)
+        us = timed(e, 840)
+        e.reset_halo_wait()
+        e.run(840)
+        p = e.pstream_phases()
+        per = [v / max(1.0, p[0]) for v in p[1:]]
+        print(f"phases {nx}x4096 K={K} cols={cols}: {us:.3f} us/step, chunk {us * K:.2f} us; per wave-chunk: "
+              + ", ".join(f"{nm} {v:.2f}" for nm, v in zip(names, per)) + f"; sum {sum(per):.2f}", flush=True)
+        del e
