@@ -323,7 +323,9 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
         tile_cpl_ = CPL;
         tile_nt_ = NT;
         Tile& T = tiles_[0];
-        const int64_t need = tile_count((int)NX, (int)NY, TX, RY - 2 * K);
+        // two partial sets: a check's partials are still read (deferred decision) by the next
+        // launch while that launch may store its own check's
+        const int64_t need = 2 * tile_count((int)NX, (int)NY, TX, RY - 2 * K);
         if (need > T.pcap) {
           hipFree(T.partials);
           T.pcap = need;
@@ -1119,6 +1121,13 @@ RunStats Engine::run_impl(int64_t steps) {
     // recomputation, so a check costs no launch of its own (interval 20 at K 16: 1.25 launches
     // per 20 steps instead of 2).
     const bool span = fused_ && recompute_rollback();
+    // span mode defers each check's decision to the next launch (TileArgs::pend): the check
+    // launch only stores its partials (set `pset` of the two), the next launch's workgroups sum
+    // them before their own work, and a check left pending at the end of the run is decided by
+    // one small kernel
+    bool pend = false;
+    int pend_n = 0, pset = 0;
+    DecideArgs pend_dec;
     while (steps_done_ < target) {
       bool check = false;
       int lvl = 0;
@@ -1152,24 +1161,41 @@ RunStats Engine::run_impl(int64_t steps) {
       a.per_x = opt_.periodic_x;
       a.per_y = opt_.periodic_y;
       a.partials = T.partials;
+      if (span && pend) {
+        a.pend = T.partials + (size_t)(pset ^ 1) * (size_t)(T.pcap / 2);
+        a.pend_n = pend_n;
+        a.pend_dec = pend_dec;
+        pend = false;
+      }
       if (fused_) {
         a.stop = d_stop_;
         if (check) {
           a.keep = recompute_rollback() ? nullptr : T.keep + T.g.idx(0, 0);
           a.rlev = lvl;
-          a.dec = decide_args(0, true);  // the last block sums the partials and decides
+          if (span) {
+            a.partials = T.partials + (size_t)pset * (size_t)(T.pcap / 2);
+            pend = true;
+            pend_n = tile_count(a.NX, a.NY, a.TX, a.TY);
+            pend_dec = decide_args(0, true);
+            pset ^= 1;
+          } else {
+            a.dec = decide_args(0, true);  // the last block sums the partials and decides
+          }
           decided_in_launch_ = true;
         }
       }
       trace_begin("step", compute_);
       launch_tile(a, opt_.precision, check, compute_);
       trace_end("step", compute_);
-      if (check && !fused_) launch_reduce_sum(T.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
+      if (check && !fused_) launch_reduce_sum(a.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
       T.cur = 1 - T.cur;
       ++st.chunks;
       if (check) {
         if (fused_) {
-          if (check_point(steps_done_, k, lvl > 0 ? lvl : k)) break;  // converged (seen by the host)
+          if (check_point(steps_done_, k, lvl > 0 ? lvl : k)) {
+            pend = false;  // seen converged: nothing later needs deciding
+            break;
+          }
         } else {
           st.residual = finish_residual();
           if (st.residual < opt_.sensitivity) {
@@ -1181,6 +1207,8 @@ RunStats Engine::run_impl(int64_t steps) {
       }
       steps_done_ += k;
     }
+    // the run's last check, not followed by a launch: decide it now
+    if (pend) launch_reduce_decide(T.partials + (size_t)(pset ^ 1) * (size_t)(T.pcap / 2), pend_n, pend_dec, compute_);
   } else if (single && opt_.small_grid_lds && !opt_.naive && lds_solver_fits(dec_.NX, dec_.NY) && steps > 0) {
     // Whole run inside one workgroup's LDS.
     st.path = "lds";

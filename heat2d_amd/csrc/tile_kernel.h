@@ -26,6 +26,14 @@ struct TileArgs {
   // check is rolled back by recomputation (keep must be null).
   int rlev = 0;
   DecideArgs dec;         // residual launches: fused sum + decision (last block)
+  // Deferred decision (fused check, lone tile): the PREVIOUS launch's check left `pend_n`
+  // residual partials at `pend`; every block of this launch sums them in one fixed order before
+  // its own work (the loads overlap its region loads) and does nothing if they converged, and
+  // block 0 records the decision (pend_dec).  The check launch itself then only stores its
+  // partials: no drain, ticket or decision on its critical path.
+  const double* pend = nullptr;
+  int pend_n = 0;
+  DecideArgs pend_dec;
 };
 size_t tile_lds_bytes(int TX, int RY, int K);
 // a lane owns up to kTileMaxSweeps region rows (kept in registers across the launch's levels)

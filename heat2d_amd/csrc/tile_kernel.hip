@@ -112,6 +112,12 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
   // unconditional load (a dummy zero word without a stop word): no branch, so no wait here
   const unsigned long long stopped =
       __hip_atomic_load(a.stop != nullptr ? a.stop : &g_tile_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the previous check's partials (deferred decision): wave 0 issues its loads before the region
+  // loads; summed below in publish_partial's order (lane-strided, then the wave butterfly)
+  double pend_s = 0.0;
+  const bool pend = live && a.pend != nullptr;
+  if (pend && tid < 64)
+    for (int i = tid; i < a.pend_n; i += 64) pend_s += a.pend[i];
   float* cur = lds;
   float* nxt = lds + RX * W;
 
@@ -140,7 +146,22 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
     for (int u = 0; u < LB; ++u)
       if (e0 + u * NT < total) cur[e0 + u * NT] = v[u];  // W == RY: region element e lives at cur[e]
   }
-  if (!live || stopped != 0ull) return;  // converged earlier: write nothing (uniform per workgroup)
+  if (!live) return;
+  if (!pend && stopped != 0ull) return;  // converged earlier (the word is stable in launches without `pend`)
+  // `pend`: block 0 sets the stop word DURING this launch, so the decision to do nothing is made
+  // once per workgroup (thread 0), shared through LDS and read after the barrier below
+  __shared__ int pend_stop;
+  if (pend && tid < 64) {
+    const double tot = wave_sum(pend_s);
+    if (tid == 0) {
+      const bool conv = tot < a.pend_dec.sens;
+      pend_stop = (stopped != 0ull || conv) ? 1 : 0;
+      if (blockIdx.x == 0 && stopped == 0ull) {
+        *a.pend_dec.total = tot;
+        decide_total(tot, a.pend_dec);  // the stop word for later launches, the host record
+      }
+    }
+  }
 
   // ---- per-thread column group and its edge masks (fixed: hold, ghost-zero: zero) ----
   const int q = tid % G;
@@ -166,6 +187,7 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
   const Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
   double racc = 0.0;
   __syncthreads();
+  if (pend && pend_stop != 0) return;  // converged: this launch is a no-op (uniform per workgroup)
 
   // ---- this lane's rows r_j = r_off + j·RSTEP (j < MJ) stay fixed for the whole launch: their
   // cells live in registers across levels (only rows r±1 are read from LDS), and their edge
@@ -221,16 +243,8 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
     nxt = tmp;
   }
 
-  // ---- write the owned tile back ----
-  const int xs = bx * a.TX, ys = by * a.TY;
-  for (int e = tid; e < a.TX * a.TY; e += NT) {
-    const int i = e / a.TY, j = e - i * a.TY;
-    if (xs + i < a.NX && ys + j < a.NY) {
-      a.dst[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + K + j];
-      // after the final swap `nxt` holds level K-1
-      if (RESID && a.keep != nullptr) a.keep[(int64_t)(xs + i) * a.pitch + (ys + j)] = nxt[(K + i) * W + K + j];
-    }
-  }
+  // ---- the residual partial first (its store and, with a ticket, the decision overlap the
+  // write-back below), then the owned tile ----
   if constexpr (RESID) {
     constexpr int NW = NT / 64;
     __shared__ double part[NW];
@@ -242,6 +256,15 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
 #pragma unroll
       for (int w = 1; w < NW; ++w) tot += part[w];
       publish_partial(a.partials, blockIdx.x, tot, a.ntiles, a.dec, tid);
+    }
+  }
+  const int xs = bx * a.TX, ys = by * a.TY;
+  for (int e = tid; e < a.TX * a.TY; e += NT) {
+    const int i = e / a.TY, j = e - i * a.TY;
+    if (xs + i < a.NX && ys + j < a.NY) {
+      a.dst[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + K + j];
+      // after the final swap `nxt` holds level K-1
+      if (RESID && a.keep != nullptr) a.keep[(int64_t)(xs + i) * a.pitch + (ys + j)] = nxt[(K + i) * W + K + j];
     }
   }
 }
