@@ -1081,325 +1081,24 @@ RunStats Engine::run_impl(int64_t steps) {
   const auto w0 = std::chrono::steady_clock::now();
   const int64_t target = steps_done_ + steps;
   tl_recs_.clear();
-
   if (!on_gpu()) {
-    st.path = "cpu";
-    while (steps_done_ < target) {
-      bool check = false;
-      const int k = next_chunk(steps_done_, target, &check);
-      if (has_exchange_) {
-        exchange_local(k);
-        ++st.exchanges;
-      }
-      advance(k, check);
-      ++st.chunks;
-      if (check) {
-        st.residual = local_residual();
-        if (st.residual < opt_.sensitivity) {
-          rollback();
-          st.converged = true;
-          break;
-        }
-      }
-      steps_done_ += k;
-    }
+    run_cpu(st, target);
     st.steps_done = steps_done_;
     st.wall_ms = st.device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     return st;
   }
-
   const bool timing = opt_.sync_mode == 0 || opt_.sync_mode == 3;
   if (timing) H2D_HIP_CHECK(hipEventRecord(ev_t0_, compute_));
   const bool single = tiles_.size() == 1 && !has_exchange_;
   if (tiled_) {
-    // LDS-tiled path: one launch per chunk of up to tile_k_ steps, the tiling re-derived per
-    // chunk length (TY = RY - 2k).
-    st.path = "tiled";
-    Tile& T = tiles_[0];
-    // A lone fused-check tile lets a chunk run THROUGH a check step: the residual is summed at
-    // that level inside the launch (TileArgs::rlev) and a converged check is rolled back by
-    // recomputation, so a check costs no launch of its own (interval 20 at K 16: 1.25 launches
-    // per 20 steps instead of 2).
-    const bool span = fused_ && recompute_rollback();
-    // span mode defers each check's decision to the next launch (TileArgs::pend): the check
-    // launch only stores its partials (set `pset` of the two), the next launch's workgroups sum
-    // them before their own work, and a check left pending at the end of the run is decided by
-    // one small kernel
-    bool pend = false;
-    int pend_n = 0, pset = 0;
-    DecideArgs pend_dec;
-    while (steps_done_ < target) {
-      bool check = false;
-      int lvl = 0;
-      int k;
-      if (span) {
-        const int64_t seg = target - steps_done_, n = (seg + tile_k_ - 1) / tile_k_;
-        const int64_t next_check = (steps_done_ / opt_.interval + 1) * opt_.interval;
-        int64_t kk = std::max<int64_t>(1, (seg + n - 1) / n);
-        kk = std::min<int64_t>(kk, next_check + opt_.interval - 1 - steps_done_);  // one check per chunk
-        k = (int)kk;
-        check = opt_.convergence && steps_done_ + k >= next_check;
-        lvl = check ? (int)(next_check - steps_done_) : 0;
-      } else {
-        k = chunk_len(steps_done_, target, tile_k_, &check);
-      }
-      TileArgs a;
-      a.src = T.buf[T.cur] + T.g.idx(0, 0);
-      a.dst = T.buf[1 - T.cur] + T.g.idx(0, 0);
-      a.pitch = T.g.pitch;
-      a.NX = (int)T.g.xcell;
-      a.NY = (int)T.g.ycell;
-      a.TX = tile_tx_;
-      a.NT = tile_nt_;
-      a.CPL = tile_cpl_;
-      a.RY = tile_ry_;
-      a.K = k;
-      a.TY = tile_ry_ - 2 * k;
-      a.cx = opt_.cx;
-      a.cy = opt_.cy;
-      a.fixed = opt_.boundary == kFixed;
-      a.per_x = opt_.periodic_x;
-      a.per_y = opt_.periodic_y;
-      a.partials = T.partials;
-      if (span && pend) {
-        a.pend = T.partials + (size_t)(pset ^ 1) * (size_t)(T.pcap / 2);
-        a.pend_n = pend_n;
-        a.pend_dec = pend_dec;
-        pend = false;
-      }
-      if (fused_) {
-        a.stop = d_stop_;
-        if (check) {
-          a.keep = recompute_rollback() ? nullptr : T.keep + T.g.idx(0, 0);
-          a.rlev = lvl;
-          if (span) {
-            a.partials = T.partials + (size_t)pset * (size_t)(T.pcap / 2);
-            pend = true;
-            pend_n = tile_count(a.NX, a.NY, a.TX, a.TY);
-            pend_dec = decide_args(0, true);
-            pset ^= 1;
-          } else {
-            a.dec = decide_args(0, true);  // the last block sums the partials and decides
-          }
-          decided_in_launch_ = true;
-        }
-      }
-      trace_begin("step", compute_);
-      launch_tile(a, opt_.precision, check, compute_);
-      trace_end("step", compute_);
-      if (check && !fused_) launch_reduce_sum(a.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
-      T.cur = 1 - T.cur;
-      ++st.chunks;
-      if (check) {
-        if (fused_) {
-          if (check_point(steps_done_, k, lvl > 0 ? lvl : k)) {
-            pend = false;  // seen converged: nothing later needs deciding
-            break;
-          }
-        } else {
-          st.residual = finish_residual();
-          if (st.residual < opt_.sensitivity) {
-            rollback();
-            st.converged = true;
-            break;
-          }
-        }
-      }
-      steps_done_ += k;
-    }
-    // the run's last check, not followed by a launch: decide it now
-    if (pend) launch_reduce_decide(T.partials + (size_t)(pset ^ 1) * (size_t)(T.pcap / 2), pend_n, pend_dec, compute_);
+    run_tiled(st, target);
   } else if (single && opt_.small_grid_lds && !opt_.naive && lds_solver_fits(dec_.NX, dec_.NY) && steps > 0) {
-    // Whole run inside one workgroup's LDS.
-    st.path = "lds";
-    Tile& T = tiles_[0];
-    const int interval = opt_.convergence ? (int)opt_.interval : 0;
-    // The LDS kernel counts steps from 1; align the convergence cadence with steps_done_.
-    if (interval > 0 && steps_done_ % interval != 0)
-      throw std::runtime_error("LDS solver: resume point must be a multiple of the convergence interval");
-    launch_lds_solver(T.buf[T.cur] + T.g.idx(0, 0), T.g.pitch, T.buf[1 - T.cur] + T.g.idx(0, 0), T.g.pitch, T.g.xcell,
-                      T.g.ycell, steps, opt_.precision, opt_.boundary, opt_.cx, opt_.cy, opt_.periodic_x,
-                      opt_.periodic_y, interval, opt_.sensitivity, d_lds_steps_, d_resid_, compute_);
-    long long done = 0;
-    H2D_HIP_CHECK(hipMemcpyAsync(&done, d_lds_steps_, sizeof(long long), hipMemcpyDeviceToHost, compute_));
-    H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, sizeof(double), hipMemcpyDeviceToHost, compute_));
-    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
-    T.cur = 1 - T.cur;
-    st.converged = done < steps;
-    st.residual = h_resid_[0];
-    steps_done_ += done;
-    st.chunks = 1;
+    run_lds(st, steps);
   } else {
     st.path = opt_.naive ? "naive" : "stream";
-    if (direct_) {
-      // Direct pipeline (IPC, 1-D row strips): ONE launch per chunk on ONE stream.  Its halo
-      // units (top / bottom unit of every column strip) first wait in the kernel until the
-      // neighbours' pushes for this chunk have landed (flags in my uncached block), read their
-      // ghost rows from my receive buffers, and as soon as their first G output rows are
-      // final they store them into the neighbours' receive buffers over xGMI, release them at
-      // system scope and bump the neighbours' flags.  No comm stream, no RCCL kernel, no
-      // host round trip: the exchange of chunk c+1 rides inside chunk c.
-      bool check = false;
-      int k = next_chunk(steps_done_, target, &check);
-      while (k > 0) {
-        if (!check) {
-          const int J = plain_run(steps_done_, target, k);
-          if (J >= 2 && pst_everywhere(k) && pplan(k) != nullptr) {
-            // a run of equal plain chunks: ONE persistent launch (the same flags and receive-
-            // buffer parities per chunk as the launches below; every rank's plan has a
-            // persistent plan at this depth, so every rank runs this chunk run the same way)
-            trace_begin("chunk", compute_);
-            launch_pstream_chunks(k, J);
-            trace_end("chunk", compute_);
-            for (int d = kN; d <= kS; ++d) {  // 1-D row strips: N / S neighbours only
-              const int pr = dec_.neighbor(tiles_[0].rank, d);
-              if (pr >= 0) ipc_need_[d] += (unsigned long long)J * (unsigned long long)pst_counts_[pr].at((size_t)k * 2 + (d == kN ? 1 : 0));
-            }
-            ipc_chunk_ += (unsigned long long)J;
-            if (J & 1) tiles_[0].cur = 1 - tiles_[0].cur;
-            st.chunks += J;
-            st.exchanges += J;
-            poll_abort();
-            steps_done_ += (int64_t)J * k;
-            k = next_chunk(steps_done_, target, &check);
-            continue;
-          }
-        }
-        trace_begin("chunk", compute_);
-        launch_chunk_tile(0, k, check, 3);
-        trace_end("chunk", compute_);
-        for (int d = 0; d < kNumDirs; ++d) {  // the neighbours' pushes this chunk, for my next one
-          const int pr = dec_.neighbor(tiles_[0].rank, d);
-          if (pr >= 0) ipc_need_[d] += (unsigned long long)ipc_counts_[pr].at((size_t)k * kNumDirs + kDirOpp[d]);
-        }
-        ++ipc_chunk_;
-        tiles_[0].cur = 1 - tiles_[0].cur;
-        ++st.chunks;
-        ++st.exchanges;
-        poll_abort();
-        if (check) {
-          if (fused_) {
-            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
-          } else {
-            st.residual = finish_residual();
-            if (st.residual < opt_.sensitivity) {
-              rollback();
-              st.converged = true;
-              break;
-            }
-          }
-        }
-        steps_done_ += k;
-        k = next_chunk(steps_done_, target, &check);
-      }
-    } else if (has_exchange_ && sig_mode_ > 0) {
-      // Signalled pipeline (per chunk c), two streams:
-      //   compute: ONE launch of every unit of chunk c, halo-dependent units first (they are
-      //            dispatched first and are short); each of them waits in the kernel until
-      //            halo(c) has landed (halo_counter_), and when done releases its rows at
-      //            system scope and bumps sig_counter_
-      //   comm   : gate (sig_counter_ >= units launched so far) -> halo exchange of chunk c+1
-      //            -> halo_counter_ = c+1
-      // The exchange starts while the interior units of chunk c are still running, no unit
-      // competes with a second stencil launch for wave slots, and the compute stream never
-      // waits on the comm stream (a cross-queue wait costs ~6 us of dispatch latency; with
-      // device_halo_wait = 0 the launch waits on an event instead).
-      bool check = false;
-      int k = next_chunk(steps_done_, target, &check);
-      if (k > 0) {
-        H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
-        H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
-        trace_begin("exchange", comm_);
-        do_exchange_async(k);
-        trace_end("exchange", comm_);
-        exchange_landed();
-        ++st.exchanges;
-      }
-      while (k > 0) {
-        if (!dev_wait_) H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
-        trace_begin("chunk", compute_);
-        for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 3);
-        trace_end("chunk", compute_);
-        for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
-        ++st.chunks;
-        poll_abort();
-        bool check_next = false;
-        const int k_next = next_chunk(steps_done_ + k, target, &check_next);
-        if (check) {
-          // nothing is in flight on the comm stream here (the exchange of chunk c completed
-          // before the chunk started), so the all-reduce is the communicator's only operation
-          if (fused_) {
-            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
-          } else {
-            st.residual = finish_residual();
-            if (st.residual < opt_.sensitivity) {
-              rollback();
-              st.converged = true;
-              break;
-            }
-          }
-        }
-        if (k_next > 0) {
-          gate_exchange();
-          trace_begin("exchange", comm_);
-          do_exchange_async(k_next);
-          trace_end("exchange", comm_);
-          exchange_landed();
-          ++st.exchanges;
-        }
-        steps_done_ += k;
-        k = k_next;
-        check = check_next;
-      }
-      H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
-      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
-    } else {
-      while (steps_done_ < target) {
-        bool check = false;
-        const int k = next_chunk(steps_done_, target, &check);
-        if (!has_exchange_ && !check && !opt_.naive) {
-          // a run of equal plain chunks: ONE persistent launch
-          const int J = plain_run(steps_done_, target, k);
-          if (J >= 2 && pplan(k) != nullptr) {
-            trace_begin("step", compute_);
-            launch_pstream_chunks(k, J);
-            trace_end("step", compute_);
-            if (J & 1) tiles_[0].cur = 1 - tiles_[0].cur;
-            st.chunks += J;
-            steps_done_ += (int64_t)J * k;
-            poll_abort();
-            continue;
-          }
-        }
-        if (has_exchange_) {
-          H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
-          H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
-          trace_begin("exchange", comm_);
-          do_exchange_async(k);
-          trace_end("exchange", comm_);
-          H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
-          H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
-          ++st.exchanges;
-        }
-        trace_begin("step", compute_);
-        advance(k, check);
-        trace_end("step", compute_);
-        ++st.chunks;
-        if (check) {
-          if (fused_) {
-            if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
-          } else {
-            st.residual = finish_residual();
-            if (st.residual < opt_.sensitivity) {
-              rollback();
-              st.converged = true;
-              break;
-            }
-          }
-        }
-        steps_done_ += k;
-      }
-    }
+    if (direct_) run_direct(st, target);
+    else if (has_exchange_ && sig_mode_ > 0) run_signal(st, target);
+    else run_serial(st, target);
   }
   end_of_run_wait(st, w0);
   poll_abort();
@@ -1407,6 +1106,326 @@ RunStats Engine::run_impl(int64_t steps) {
   trace_collect(st);
   st.steps_done = steps_done_;
   return st;
+}
+
+// CPU: the same chunk / check schedule, halos copied between the process's tiles.
+void Engine::run_cpu(RunStats& st, int64_t target) {
+  while (steps_done_ < target) {
+    bool check = false;
+    const int k = next_chunk(steps_done_, target, &check);
+    if (has_exchange_) {
+      exchange_local(k);
+      ++st.exchanges;
+    }
+    advance(k, check);
+    ++st.chunks;
+    if (check) {
+      st.residual = local_residual();
+      if (st.residual < opt_.sensitivity) {
+        rollback();
+        st.converged = true;
+        break;
+      }
+    }
+    steps_done_ += k;
+  }
+  st.path = "cpu";
+}
+
+void Engine::run_tiled(RunStats& st, int64_t target) {
+  // LDS-tiled path: one launch per chunk of up to tile_k_ steps, the tiling re-derived per
+  // chunk length (TY = RY - 2k).
+  st.path = "tiled";
+  Tile& T = tiles_[0];
+  // A lone fused-check tile lets a chunk run THROUGH a check step: the residual is summed at
+  // that level inside the launch (TileArgs::rlev) and a converged check is rolled back by
+  // recomputation, so a check costs no launch of its own (interval 20 at K 16: 1.25 launches
+  // per 20 steps instead of 2).
+  const bool span = fused_ && recompute_rollback();
+  // span mode defers each check's decision to the next launch (TileArgs::pend): the check
+  // launch only stores its partials (set `pset` of the two), the next launch's workgroups sum
+  // them before their own work, and a check left pending at the end of the run is decided by
+  // one small kernel
+  bool pend = false;
+  int pend_n = 0, pset = 0;
+  DecideArgs pend_dec;
+  while (steps_done_ < target) {
+    bool check = false;
+    int lvl = 0;
+    int k;
+    if (span) {
+      const int64_t seg = target - steps_done_, n = (seg + tile_k_ - 1) / tile_k_;
+      const int64_t next_check = (steps_done_ / opt_.interval + 1) * opt_.interval;
+      int64_t kk = std::max<int64_t>(1, (seg + n - 1) / n);
+      kk = std::min<int64_t>(kk, next_check + opt_.interval - 1 - steps_done_);  // one check per chunk
+      k = (int)kk;
+      check = opt_.convergence && steps_done_ + k >= next_check;
+      lvl = check ? (int)(next_check - steps_done_) : 0;
+    } else {
+      k = chunk_len(steps_done_, target, tile_k_, &check);
+    }
+    TileArgs a;
+    a.src = T.buf[T.cur] + T.g.idx(0, 0);
+    a.dst = T.buf[1 - T.cur] + T.g.idx(0, 0);
+    a.pitch = T.g.pitch;
+    a.NX = (int)T.g.xcell;
+    a.NY = (int)T.g.ycell;
+    a.TX = tile_tx_;
+    a.NT = tile_nt_;
+    a.CPL = tile_cpl_;
+    a.RY = tile_ry_;
+    a.K = k;
+    a.TY = tile_ry_ - 2 * k;
+    a.cx = opt_.cx;
+    a.cy = opt_.cy;
+    a.fixed = opt_.boundary == kFixed;
+    a.per_x = opt_.periodic_x;
+    a.per_y = opt_.periodic_y;
+    a.partials = T.partials;
+    if (span && pend) {
+      a.pend = T.partials + (size_t)(pset ^ 1) * (size_t)(T.pcap / 2);
+      a.pend_n = pend_n;
+      a.pend_dec = pend_dec;
+      pend = false;
+    }
+    if (fused_) {
+      a.stop = d_stop_;
+      if (check) {
+        a.keep = recompute_rollback() ? nullptr : T.keep + T.g.idx(0, 0);
+        a.rlev = lvl;
+        if (span) {
+          a.partials = T.partials + (size_t)pset * (size_t)(T.pcap / 2);
+          pend = true;
+          pend_n = tile_count(a.NX, a.NY, a.TX, a.TY);
+          pend_dec = decide_args(0, true);
+          pset ^= 1;
+        } else {
+          a.dec = decide_args(0, true);  // the last block sums the partials and decides
+        }
+        decided_in_launch_ = true;
+      }
+    }
+    trace_begin("step", compute_);
+    launch_tile(a, opt_.precision, check, compute_);
+    trace_end("step", compute_);
+    if (check && !fused_) launch_reduce_sum(a.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
+    T.cur = 1 - T.cur;
+    ++st.chunks;
+    if (check) {
+      if (fused_) {
+        if (check_point(steps_done_, k, lvl > 0 ? lvl : k)) {
+          pend = false;  // seen converged: nothing later needs deciding
+          break;
+        }
+      } else {
+        st.residual = finish_residual();
+        if (st.residual < opt_.sensitivity) {
+          rollback();
+          st.converged = true;
+          break;
+        }
+      }
+    }
+    steps_done_ += k;
+  }
+  // the run's last check, not followed by a launch: decide it now
+  if (pend) launch_reduce_decide(T.partials + (size_t)(pset ^ 1) * (size_t)(T.pcap / 2), pend_n, pend_dec, compute_);
+}
+
+void Engine::run_lds(RunStats& st, int64_t steps) {
+  // Whole run inside one workgroup's LDS.
+  st.path = "lds";
+  Tile& T = tiles_[0];
+  const int interval = opt_.convergence ? (int)opt_.interval : 0;
+  // The LDS kernel counts steps from 1; align the convergence cadence with steps_done_.
+  if (interval > 0 && steps_done_ % interval != 0)
+    throw std::runtime_error("LDS solver: resume point must be a multiple of the convergence interval");
+  launch_lds_solver(T.buf[T.cur] + T.g.idx(0, 0), T.g.pitch, T.buf[1 - T.cur] + T.g.idx(0, 0), T.g.pitch, T.g.xcell,
+                    T.g.ycell, steps, opt_.precision, opt_.boundary, opt_.cx, opt_.cy, opt_.periodic_x,
+                    opt_.periodic_y, interval, opt_.sensitivity, d_lds_steps_, d_resid_, compute_);
+  long long done = 0;
+  H2D_HIP_CHECK(hipMemcpyAsync(&done, d_lds_steps_, sizeof(long long), hipMemcpyDeviceToHost, compute_));
+  H2D_HIP_CHECK(hipMemcpyAsync(h_resid_, d_resid_, sizeof(double), hipMemcpyDeviceToHost, compute_));
+  H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+  T.cur = 1 - T.cur;
+  st.converged = done < steps;
+  st.residual = h_resid_[0];
+  steps_done_ += done;
+  st.chunks = 1;
+}
+
+void Engine::run_direct(RunStats& st, int64_t target) {
+  // Direct pipeline (IPC, 1-D row strips): ONE launch per chunk on ONE stream.  Its halo
+  // units (top / bottom unit of every column strip) first wait in the kernel until the
+  // neighbours' pushes for this chunk have landed (flags in my uncached block), read their
+  // ghost rows from my receive buffers, and as soon as their first G output rows are
+  // final they store them into the neighbours' receive buffers over xGMI, release them at
+  // system scope and bump the neighbours' flags.  No comm stream, no RCCL kernel, no
+  // host round trip: the exchange of chunk c+1 rides inside chunk c.
+  bool check = false;
+  int k = next_chunk(steps_done_, target, &check);
+  while (k > 0) {
+    if (!check) {
+      const int J = plain_run(steps_done_, target, k);
+      if (J >= 2 && pst_everywhere(k) && pplan(k) != nullptr) {
+        // a run of equal plain chunks: ONE persistent launch (the same flags and receive-
+        // buffer parities per chunk as the launches below; every rank's plan has a
+        // persistent plan at this depth, so every rank runs this chunk run the same way)
+        trace_begin("chunk", compute_);
+        launch_pstream_chunks(k, J);
+        trace_end("chunk", compute_);
+        for (int d = kN; d <= kS; ++d) {  // 1-D row strips: N / S neighbours only
+          const int pr = dec_.neighbor(tiles_[0].rank, d);
+          if (pr >= 0) ipc_need_[d] += (unsigned long long)J * (unsigned long long)pst_counts_[pr].at((size_t)k * 2 + (d == kN ? 1 : 0));
+        }
+        ipc_chunk_ += (unsigned long long)J;
+        if (J & 1) tiles_[0].cur = 1 - tiles_[0].cur;
+        st.chunks += J;
+        st.exchanges += J;
+        poll_abort();
+        steps_done_ += (int64_t)J * k;
+        k = next_chunk(steps_done_, target, &check);
+        continue;
+      }
+    }
+    trace_begin("chunk", compute_);
+    launch_chunk_tile(0, k, check, 3);
+    trace_end("chunk", compute_);
+    for (int d = 0; d < kNumDirs; ++d) {  // the neighbours' pushes this chunk, for my next one
+      const int pr = dec_.neighbor(tiles_[0].rank, d);
+      if (pr >= 0) ipc_need_[d] += (unsigned long long)ipc_counts_[pr].at((size_t)k * kNumDirs + kDirOpp[d]);
+    }
+    ++ipc_chunk_;
+    tiles_[0].cur = 1 - tiles_[0].cur;
+    ++st.chunks;
+    ++st.exchanges;
+    poll_abort();
+    if (check) {
+      if (fused_) {
+        if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+      } else {
+        st.residual = finish_residual();
+        if (st.residual < opt_.sensitivity) {
+          rollback();
+          st.converged = true;
+          break;
+        }
+      }
+    }
+    steps_done_ += k;
+    k = next_chunk(steps_done_, target, &check);
+  }
+}
+
+void Engine::run_signal(RunStats& st, int64_t target) {
+  // Signalled pipeline (per chunk c), two streams:
+  //   compute: ONE launch of every unit of chunk c, halo-dependent units first (they are
+  //            dispatched first and are short); each of them waits in the kernel until
+  //            halo(c) has landed (halo_counter_), and when done releases its rows at
+  //            system scope and bumps sig_counter_
+  //   comm   : gate (sig_counter_ >= units launched so far) -> halo exchange of chunk c+1
+  //            -> halo_counter_ = c+1
+  // The exchange starts while the interior units of chunk c are still running, no unit
+  // competes with a second stencil launch for wave slots, and the compute stream never
+  // waits on the comm stream (a cross-queue wait costs ~6 us of dispatch latency; with
+  // device_halo_wait = 0 the launch waits on an event instead).
+  bool check = false;
+  int k = next_chunk(steps_done_, target, &check);
+  if (k > 0) {
+    H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
+    H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+    trace_begin("exchange", comm_);
+    do_exchange_async(k);
+    trace_end("exchange", comm_);
+    exchange_landed();
+    ++st.exchanges;
+  }
+  while (k > 0) {
+    if (!dev_wait_) H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+    trace_begin("chunk", compute_);
+    for (int t = 0; t < (int)tiles_.size(); ++t) launch_chunk_tile(t, k, check, 3);
+    trace_end("chunk", compute_);
+    for (Tile& tl : tiles_) tl.cur = 1 - tl.cur;
+    ++st.chunks;
+    poll_abort();
+    bool check_next = false;
+    const int k_next = next_chunk(steps_done_ + k, target, &check_next);
+    if (check) {
+      // nothing is in flight on the comm stream here (the exchange of chunk c completed
+      // before the chunk started), so the all-reduce is the communicator's only operation
+      if (fused_) {
+        if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+      } else {
+        st.residual = finish_residual();
+        if (st.residual < opt_.sensitivity) {
+          rollback();
+          st.converged = true;
+          break;
+        }
+      }
+    }
+    if (k_next > 0) {
+      gate_exchange();
+      trace_begin("exchange", comm_);
+      do_exchange_async(k_next);
+      trace_end("exchange", comm_);
+      exchange_landed();
+      ++st.exchanges;
+    }
+    steps_done_ += k;
+    k = k_next;
+    check = check_next;
+  }
+  H2D_HIP_CHECK(hipEventRecord(ev_ready_, comm_));
+  H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_ready_, 0));
+}
+
+void Engine::run_serial(RunStats& st, int64_t target) {
+  while (steps_done_ < target) {
+    bool check = false;
+    const int k = next_chunk(steps_done_, target, &check);
+    if (!has_exchange_ && !check && !opt_.naive) {
+      // a run of equal plain chunks: ONE persistent launch
+      const int J = plain_run(steps_done_, target, k);
+      if (J >= 2 && pplan(k) != nullptr) {
+        trace_begin("step", compute_);
+        launch_pstream_chunks(k, J);
+        trace_end("step", compute_);
+        if (J & 1) tiles_[0].cur = 1 - tiles_[0].cur;
+        st.chunks += J;
+        steps_done_ += (int64_t)J * k;
+        poll_abort();
+        continue;
+      }
+    }
+    if (has_exchange_) {
+      H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
+      H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
+      trace_begin("exchange", comm_);
+      do_exchange_async(k);
+      trace_end("exchange", comm_);
+      H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
+      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+      ++st.exchanges;
+    }
+    trace_begin("step", compute_);
+    advance(k, check);
+    trace_end("step", compute_);
+    ++st.chunks;
+    if (check) {
+      if (fused_) {
+        if (check_point(steps_done_, k)) break;  // converged (seen by the host): stop enqueueing
+      } else {
+        st.residual = finish_residual();
+        if (st.residual < opt_.sensitivity) {
+          rollback();
+          st.converged = true;
+          break;
+        }
+      }
+    }
+    steps_done_ += k;
+  }
 }
 
 // ---- persistent pipelined stencil ----------------------------------------------------------

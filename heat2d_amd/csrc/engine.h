@@ -279,6 +279,14 @@ class Engine {
   void progress_tick(hipStream_t s);
   int chunk_len(int64_t done, int64_t total, int kmax, bool* check) const;  // convergence-aligned chunk
   RunStats run_impl(int64_t steps);
+  // the time loop of each path (run_impl picks one; each advances steps_done_ to `target` or to a
+  // converged check)
+  void run_cpu(RunStats& st, int64_t target);
+  void run_tiled(RunStats& st, int64_t target);
+  void run_lds(RunStats& st, int64_t steps);
+  void run_direct(RunStats& st, int64_t target);
+  void run_signal(RunStats& st, int64_t target);
+  void run_serial(RunStats& st, int64_t target);
   CopyDesc* local_descs(int K, int& n, int64_t& maxe);
   void check_tile(int t) const;
   void trace_begin(const char* phase, hipStream_t s);

@@ -464,6 +464,31 @@ def test_fused_convergence_matches_oracle(native, gpu, gx, gy, pipeline):
                     first = (9 * i, int(b2.sum()), int(r2.min()), int(r2.max()), int(c2.min()), int(c2.max()))
                     break
             print(f"rerun: first wrong (steps, cells, rows, cols) {first}", flush=True)
+
+            def ranges(v):
+                v = sorted(set(int(x) for x in v))
+                out, a = [], None
+                for i, x in enumerate(v):
+                    if a is None:
+                        a = x
+                    if i + 1 == len(v) or v[i + 1] != x + 1:
+                        out.append(f"{a}-{x}" if a != x else f"{a}")
+                        a = None
+                return ",".join(out[:12]) + ("..." if len(out) > 12 else "")
+
+            for conv_on in (True, False):
+                for nsteps in (1, 2, 8, 9):
+                    kw3 = {**CONV, "sensitivity": 0.0} if conv_on else {}
+                    e3 = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
+                                       small_grid_lds=False, tiled=0, **PIPELINES[pipeline], **kw3)
+                    e3.run(nsteps)
+                    g3 = _gather(e3, nx, ny)
+                    o3 = oracle(native, nx, ny, nsteps, 1)["grid"]
+                    b3 = g3 != o3
+                    r3, c3 = np.nonzero(b3)
+                    print(f"diag conv={conv_on} steps={nsteps}: wrong {int(b3.sum())} rows {ranges(r3)} cols {ranges(c3)}"
+                          + (f" max|d| {np.abs(g3 - o3).max():.4g}" if b3.any() else ""), flush=True)
+                    del e3
             pytest.fail(f"fused={fused}: converged {st['converged']} steps {st['steps_done']} residual "
                         f"{st['residual']!r} (oracle {ref['residual']!r}); grid cells != oracle: {int(bad.sum())}"
                         + (f" rows {r.min()}-{r.max()} cols {c.min()}-{c.max()} nan {int(np.isnan(got).sum())}"

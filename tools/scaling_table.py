@@ -36,7 +36,7 @@ def table(recs):
     recs = sorted(recs, key=lambda r: r["n_gpus"])
     base = next((r for r in recs if r["n_gpus"] == 1), None)
     print(f"{'GPUs':>4} {'grid':>14} {'ms/step':>9} {'cell-updates/s':>15} {'speedup':>8} {'eff.':>6} "
-          f"{'in-job S':>8} {'in-job E':>8}  transport/pipeline")
+          f"{'in-job S':>8} {'in-job E':>8} {'halo wait':>9}  transport/pipeline")
     for r in recs:
         g = r.get("config", {}).get("grid", ["?", "?"])
         if base:
@@ -50,9 +50,12 @@ def table(recs):
             s = e = float("nan")
         js, je = r.get("speedup"), r.get("efficiency")
         tp = f"{r.get('config', {}).get('transport', '')}/{r.get('config', {}).get('pipeline', '')}"
+        # exposed halo wait as a share of a chunk (the reference's MPI_Waitall share, Report p.34-37)
+        hw = (r.get("halo_wait") or {}).get("share_of_chunk")
+        hws = f"{100 * hw:8.1f}%" if hw is not None else f"{'-':>9}"
         print(f"{r['n_gpus']:>4} {str(g[0]) + 'x' + str(g[1]):>14} {r['ms_per_step']:9.4f} {r['value']:15.4e} "
               f"{s:8.2f} {e:6.2f} {js if js is not None else float('nan'):8.2f} "
-              f"{je if je is not None else float('nan'):8.2f}  {tp}")
+              f"{je if je is not None else float('nan'):8.2f} {hws}  {tp}")
 
 
 if __name__ == "__main__":
