@@ -175,23 +175,23 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     d_dummy_ = dmalloc<float>(4 * kWaveCols);
     if (o.phase_timers) {
       d_phase_ = dmalloc<unsigned long long>(kPhases);
-      H2D_HIP_CHECK(hipMemset(d_phase_, 0, kPhases * sizeof(unsigned long long)));
+      dzero(d_phase_, kPhases * sizeof(unsigned long long));
     }
     d_wait_acc_ = dmalloc<unsigned long long>(4);
-    H2D_HIP_CHECK(hipMemset(d_wait_acc_, 0, 4 * sizeof(unsigned long long)));
+    dzero(d_wait_acc_, 4 * sizeof(unsigned long long));
     if (o.timeline > 0) {
       if (o.timeline > 4096) throw std::invalid_argument("timeline: at most 4096 launches");
       d_stamps_ = dmalloc<unsigned long long>((size_t)o.timeline * kTimelineUnits * 4);
     }
     if (o.convergence && !o.naive && transport_ != kTransportExternal && o.fused_check != 0) {
       d_stop_ = dmalloc<unsigned long long>(1);
-      H2D_HIP_CHECK(hipMemset(d_stop_, 0, sizeof(unsigned long long)));
+      dzero(d_stop_, sizeof(unsigned long long));
       H2D_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_conv_), sizeof(ConvHost), hipHostMallocMapped));
       std::memset(h_conv_, 0, sizeof(ConvHost));
       H2D_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_conv_dev_), h_conv_, 0));
       H2D_HIP_CHECK(hipEventCreateWithFlags(&ev_check_, hipEventDisableTiming));
       d_ticket_ = dmalloc<unsigned int>(ranks.size());
-      H2D_HIP_CHECK(hipMemset(d_ticket_, 0, ranks.size() * sizeof(unsigned int)));
+      dzero(d_ticket_, ranks.size() * sizeof(unsigned int));
     }
   }
 
@@ -238,7 +238,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     }
     // Bounded device waits report through these (direct and signalled pipelines).
     d_sig_timeout_ = dmalloc<unsigned int>(1);
-    H2D_HIP_CHECK(hipMemset(d_sig_timeout_, 0, sizeof(unsigned int)));
+    dzero(d_sig_timeout_, sizeof(unsigned int));
     H2D_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_timeout_), sizeof(unsigned int), hipHostMallocMapped));
     *h_timeout_ = 0u;
     H2D_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_timeout_dev_), h_timeout_, 0));
@@ -262,11 +262,11 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       if (sig_mode_ == 2) {
         sig_counter_ = dmalloc<unsigned long long>(8);
       }
-      H2D_HIP_CHECK(hipMemset(sig_counter_, 0, sizeof(unsigned long long)));
+      dzero(sig_counter_, sizeof(unsigned long long));
       dev_wait_ = opt_.device_halo_wait != 0;
       if (dev_wait_) {
         halo_counter_ = dmalloc<unsigned long long>(8);
-        H2D_HIP_CHECK(hipMemset(halo_counter_, 0, sizeof(unsigned long long)));
+        dzero(halo_counter_, sizeof(unsigned long long));
       }
     }
     // every unit list up front (a direct plan that cannot be built fails here, before any
@@ -568,13 +568,13 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     L.d_all = dmalloc<Unit>(all.size());
     L.d_interior = dmalloc<Unit>(in.size());
     L.d_boundary = dmalloc<Unit>(bd.size());
-    H2D_HIP_CHECK(hipMemcpy(L.d_all, all.data(), all.size() * sizeof(Unit), hipMemcpyHostToDevice));
-    if (!in.empty()) H2D_HIP_CHECK(hipMemcpy(L.d_interior, in.data(), in.size() * sizeof(Unit), hipMemcpyHostToDevice));
-    if (!bd.empty()) H2D_HIP_CHECK(hipMemcpy(L.d_boundary, bd.data(), bd.size() * sizeof(Unit), hipMemcpyHostToDevice));
+    h2d(L.d_all, all.data(), all.size() * sizeof(Unit));
+    if (!in.empty()) h2d(L.d_interior, in.data(), in.size() * sizeof(Unit));
+    if (!bd.empty()) h2d(L.d_boundary, bd.data(), bd.size() * sizeof(Unit));
     std::vector<Unit> bfirst = bd;
     bfirst.insert(bfirst.end(), in.begin(), in.end());
     L.d_bfirst = dmalloc<Unit>(bfirst.size());
-    H2D_HIP_CHECK(hipMemcpy(L.d_bfirst, bfirst.data(), bfirst.size() * sizeof(Unit), hipMemcpyHostToDevice));
+    h2d(L.d_bfirst, bfirst.data(), bfirst.size() * sizeof(Unit));
     Tile& tw = tiles_[t];
     if ((int64_t)all.size() > tw.pcap) {
       H2D_HIP_CHECK(hipDeviceSynchronize());
@@ -792,7 +792,7 @@ CopyDesc* Engine::local_descs(int K, int& n, int64_t& maxe) {
     CopyDesc* dd = nullptr;
     if (on_gpu() && !v.empty()) {
       dd = dmalloc<CopyDesc>(v.size());
-      H2D_HIP_CHECK(hipMemcpy(dd, v.data(), v.size() * sizeof(CopyDesc), hipMemcpyHostToDevice));
+      h2d(dd, v.data(), v.size() * sizeof(CopyDesc));
     } else if (!on_gpu()) {
       // CPU: keep the host descriptors alive in a heap block.
       dd = new CopyDesc[v.size() ? v.size() : 1];
@@ -818,13 +818,14 @@ void Engine::exchange_local(int k) {
   }
 }
 
-void Engine::do_exchange_async(int K) {
-  // Runs on comm_ after ev_ready_.
+void Engine::do_exchange_async(int K, hipStream_t s) {
+  // Runs on comm_ after ev_ready_ (or, serial pipeline, in order on the compute stream).
+  hipStream_t xs = s ? s : comm_;
   if (transport_ == kTransportLocal) {
     int n = 0;
     int64_t me = 0;
     CopyDesc* d = local_descs(K, n, me);
-    launch_copy_rects(d, n, me, comm_);
+    launch_copy_rects(d, n, me, xs);
     return;
   }
   if (transport_ != kTransportRccl) throw std::logic_error("do_exchange_async: transport");
@@ -844,20 +845,20 @@ void Engine::do_exchange_async(int K) {
     auto row = [&](int64_t i) { return b + (size_t)(i + g.G) * (size_t)g.pitch; };
     H2D_NCCL_CHECK(ncclGroupStart());
     for (int d = 0; d < kNumDirs; ++d) {
-      if (d == kN && pn >= 0) H2D_NCCL_CHECK(ncclSend(row(0), cnt, ncclFloat, pn, comm, comm_));
-      if (d == kS && ps >= 0) H2D_NCCL_CHECK(ncclSend(row(g.xcell - K), cnt, ncclFloat, ps, comm, comm_));
+      if (d == kN && pn >= 0) H2D_NCCL_CHECK(ncclSend(row(0), cnt, ncclFloat, pn, comm, xs));
+      if (d == kS && ps >= 0) H2D_NCCL_CHECK(ncclSend(row(g.xcell - K), cnt, ncclFloat, ps, comm, xs));
     }
     for (int d = 0; d < kNumDirs; ++d) {
       const int gs = kDirOpp[d];
-      if (gs == kN && pn >= 0) H2D_NCCL_CHECK(ncclRecv(row(-K), cnt, ncclFloat, pn, comm, comm_));
-      if (gs == kS && ps >= 0) H2D_NCCL_CHECK(ncclRecv(row(g.xcell), cnt, ncclFloat, ps, comm, comm_));
+      if (gs == kN && pn >= 0) H2D_NCCL_CHECK(ncclRecv(row(-K), cnt, ncclFloat, pn, comm, xs));
+      if (gs == kS && ps >= 0) H2D_NCCL_CHECK(ncclRecv(row(g.xcell), cnt, ncclFloat, ps, comm, xs));
     }
     H2D_NCCL_CHECK(ncclGroupEnd());
     return;
   }
   ExchangePlan p = make_plan(dec_, T.rank, T.g, K);
   if (p.send_total > stage_cap_ || p.recv_total > stage_cap_) {
-    H2D_HIP_CHECK(hipStreamSynchronize(comm_));
+    H2D_HIP_CHECK(hipStreamSynchronize(xs));
     hipFree(d_send_);
     hipFree(d_recv_);
     stage_cap_ = std::max(p.send_total, p.recv_total);
@@ -878,28 +879,28 @@ void Engine::do_exchange_async(int K) {
     for (auto& c : pv) me = std::max(me, c.rows * c.cols);
     CopyDesc* dp = dmalloc<CopyDesc>(pv.size());
     CopyDesc* du = dmalloc<CopyDesc>(uv.size());
-    if (!pv.empty()) H2D_HIP_CHECK(hipMemcpy(dp, pv.data(), pv.size() * sizeof(CopyDesc), hipMemcpyHostToDevice));
-    if (!uv.empty()) H2D_HIP_CHECK(hipMemcpy(du, uv.data(), uv.size() * sizeof(CopyDesc), hipMemcpyHostToDevice));
+    if (!pv.empty()) h2d(dp, pv.data(), pv.size() * sizeof(CopyDesc));
+    if (!uv.empty()) h2d(du, uv.data(), uv.size() * sizeof(CopyDesc));
     ip = pack_descs_.emplace(key, std::make_tuple(dp, (int)pv.size(), me)).first;
     unpack_descs_.emplace(key, std::make_tuple(du, (int)uv.size(), me));
   }
   auto iu = unpack_descs_.find(key);
-  launch_copy_rects(std::get<0>(ip->second), std::get<1>(ip->second), std::get<2>(ip->second), comm_);
+  launch_copy_rects(std::get<0>(ip->second), std::get<1>(ip->second), std::get<2>(ip->second), xs);
   H2D_NCCL_CHECK(ncclGroupStart());
   // Send segment d to peer[d]; receive the peer's matching segment into ghost side opp(d)
   // from peer[opp(d)].  Posting both in direction order keeps per-peer FIFO matching
   // correct even when one peer is the neighbour on several sides (periodic, 2-wide grids).
   for (int d = 0; d < kNumDirs; ++d) {
     if (p.peer[d] < 0 || p.send_rect[d].count() == 0) continue;
-    H2D_NCCL_CHECK(ncclSend(d_send_ + p.send_off[d], (size_t)p.send_rect[d].count(), ncclFloat, p.peer[d], comm, comm_));
+    H2D_NCCL_CHECK(ncclSend(d_send_ + p.send_off[d], (size_t)p.send_rect[d].count(), ncclFloat, p.peer[d], comm, xs));
   }
   for (int d = 0; d < kNumDirs; ++d) {
     const int g = kDirOpp[d];
     if (p.peer[g] < 0 || p.recv_rect[g].count() == 0) continue;
-    H2D_NCCL_CHECK(ncclRecv(d_recv_ + p.recv_off[g], (size_t)p.recv_rect[g].count(), ncclFloat, p.peer[g], comm, comm_));
+    H2D_NCCL_CHECK(ncclRecv(d_recv_ + p.recv_off[g], (size_t)p.recv_rect[g].count(), ncclFloat, p.peer[g], comm, xs));
   }
   H2D_NCCL_CHECK(ncclGroupEnd());
-  launch_copy_rects(std::get<0>(iu->second), std::get<1>(iu->second), std::get<2>(iu->second), comm_);
+  launch_copy_rects(std::get<0>(iu->second), std::get<1>(iu->second), std::get<2>(iu->second), xs);
 }
 
 void Engine::gate_exchange() {
@@ -1399,13 +1400,12 @@ void Engine::run_serial(RunStats& st, int64_t target) {
       }
     }
     if (has_exchange_) {
-      H2D_HIP_CHECK(hipEventRecord(ev_ready_, compute_));
-      H2D_HIP_CHECK(hipStreamWaitEvent(comm_, ev_ready_, 0));
-      trace_begin("exchange", comm_);
-      do_exchange_async(k);
-      trace_end("exchange", comm_);
-      H2D_HIP_CHECK(hipEventRecord(ev_halo_, comm_));
-      H2D_HIP_CHECK(hipStreamWaitEvent(compute_, ev_halo_, 0));
+      // serial: nothing overlaps the exchange, so it runs in order on the compute stream (no
+      // cross-stream event pair per chunk: the GPU test suite saw this pipeline compute a wrong
+      // tile now and then in a process holding many streams, never with one stream)
+      trace_begin("exchange", compute_);
+      do_exchange_async(k, compute_);
+      trace_end("exchange", compute_);
       ++st.exchanges;
     }
     trace_begin("step", compute_);
@@ -1489,9 +1489,9 @@ const Engine::PPlan* Engine::pplan(int K) {
   }
   if (P.n > 0) {
     P.d_units = dmalloc<PUnit>((size_t)P.n);
-    H2D_HIP_CHECK(hipMemcpy(P.d_units, P.host.data(), (size_t)P.n * sizeof(PUnit), hipMemcpyHostToDevice));
+    h2d(P.d_units, P.host.data(), (size_t)P.n * sizeof(PUnit));
     P.d_prog = dmalloc<unsigned>((size_t)P.n * 32);
-    H2D_HIP_CHECK(hipMemset(P.d_prog, 0, (size_t)P.n * 32 * sizeof(unsigned)));
+    dzero(P.d_prog, (size_t)P.n * 32 * sizeof(unsigned));
   }
   auto& ref = pplans_.emplace(K, std::move(P)).first->second;
   return ref.n > 0 ? &ref : nullptr;
@@ -1767,6 +1767,24 @@ void Engine::unpack(int t, int k, uintptr_t recvbuf) {
   }
 }
 
+void Engine::dzero(void* p, size_t bytes) const {
+  // zeroing ordered on the compute stream (a hipMemset may complete after a kernel of the
+  // non-blocking compute stream has already read the old bytes: see Engine::h2d)
+  H2D_HIP_CHECK(hipMemsetAsync(p, 0, bytes, compute_));
+}
+
+void Engine::h2d(void* dst, const void* src, size_t bytes) const {
+  // Host -> device copy of a plan (unit lists, copy descriptors, IPC pointers): ordered on the
+  // compute stream and complete on return.  A blocking hipMemcpy from pageable memory may return
+  // before its DMA has landed, and the compute stream does not wait for the null stream
+  // (hipStreamNonBlocking): a kernel enqueued next could read the previous bytes of a reused
+  // allocation — seen in the GPU suite as whole unit bands computed wrong, in processes that had
+  // freed many engines.
+  if (bytes == 0) return;
+  H2D_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, compute_));
+  H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+}
+
 std::vector<float> Engine::download(int t) const {
   check_tile(t);
   const Tile& T = tiles_[t];
@@ -1787,9 +1805,11 @@ void Engine::upload(int t, const float* owned) {
   Tile& T = tiles_[t];
   if (direct_) ipc_primed_ = false;  // the neighbours must receive the new boundary rows
   if (on_gpu()) {
+    // ordered on the compute stream and complete on return (see Engine::h2d)
+    H2D_HIP_CHECK(hipMemcpy2DAsync(T.buf[T.cur] + T.g.idx(0, 0), T.g.pitch * sizeof(float), owned,
+                                   T.g.ycell * sizeof(float), T.g.ycell * sizeof(float), T.g.xcell,
+                                   hipMemcpyHostToDevice, compute_));
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
-    H2D_HIP_CHECK(hipMemcpy2D(T.buf[T.cur] + T.g.idx(0, 0), T.g.pitch * sizeof(float), owned, T.g.ycell * sizeof(float),
-                              T.g.ycell * sizeof(float), T.g.xcell, hipMemcpyHostToDevice));
   } else {
     for (int64_t i = 0; i < T.g.xcell; ++i)
       std::memcpy(T.buf[T.cur] + T.g.idx(i, 0), owned + i * T.g.ycell, T.g.ycell * sizeof(float));
@@ -1818,8 +1838,8 @@ Engine::HaloWait Engine::halo_wait() const {
 void Engine::reset_halo_wait() {
   if (!on_gpu()) return;
   synchronize();
-  H2D_HIP_CHECK(hipMemset(d_wait_acc_, 0, 4 * sizeof(unsigned long long)));
-  if (d_phase_) H2D_HIP_CHECK(hipMemset(d_phase_, 0, kPhases * sizeof(unsigned long long)));
+  dzero(d_wait_acc_, 4 * sizeof(unsigned long long));
+  if (d_phase_) dzero(d_phase_, kPhases * sizeof(unsigned long long));
 }
 
 std::vector<double> Engine::pstream_phases() const {
@@ -2005,7 +2025,7 @@ void Engine::ipc_open(const std::vector<std::string>& handles) {
     H2D_HIP_CHECK(hipMemcpy(&probe, ipc_blocks_[r], sizeof(probe), hipMemcpyDeviceToHost));
   }
   d_ipc_blocks_ = dmalloc<char*>((size_t)nr);
-  H2D_HIP_CHECK(hipMemcpy(d_ipc_blocks_, ipc_blocks_.data(), nr * sizeof(char*), hipMemcpyHostToDevice));
+  h2d(d_ipc_blocks_, ipc_blocks_.data(), nr * sizeof(char*));
   ipc_primed_ = false;
 }
 

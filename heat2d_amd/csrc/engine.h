@@ -267,7 +267,9 @@ class Engine {
   // read (-1: current)
   void launch_chunk_tile(int t, int K, bool residual, int which, int src = -1, hipStream_t stream = nullptr);
   void reduce_tile_residual(int t, int K);
-  void do_exchange_async(int K);  // enqueue on comm stream
+  void do_exchange_async(int K, hipStream_t s = nullptr);
+  void h2d(void* dst, const void* src, size_t bytes) const;  // plan upload, complete on return
+  void dzero(void* p, size_t bytes) const;  // zero, ordered on the compute stream  // enqueue on `s` (default: the comm stream)
   double finish_residual();       // reduce + (rccl) all-reduce, host sync
   void wait_event(hipEvent_t ev);  // blocking wait with RCCL error polling + progress watchdog
   // Progress events for the watchdog: every 16th launch records one (ring of 8); a wait resets

@@ -44,6 +44,7 @@ for s in "$@"; do
     pcols) step pcols 400 python -u tools/pstream_check.py cols ;;
     pphases) step pphases 300 python -u tools/pstream_check.py phases ;;
     profconv) step profconv 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profconv -o run -- python tools/conv_probe.py 80x64 ;;
+    stress) step stress 400 python -u tools/stress_flaky.py 30 ;;
     pksweep) step pksweep 300 python -u tools/pstream_check.py ksweep ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;
