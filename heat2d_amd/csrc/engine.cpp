@@ -337,7 +337,9 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     if (!opt_.naive && (opt_.persistent > 0 || (opt_.persistent < 0 && direct_)))
       warm_pstream_kernels(opt_.precision, G_, compute_);
     if (tiled_) warm_tile_kernels(opt_.precision, compute_);
-    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    // the whole device, not only this engine's stream: nothing another stream or the null stream
+    // still has in flight (copies, fills of reused allocations) may overlap the first chunk
+    H2D_HIP_CHECK(hipDeviceSynchronize());
   }
 }
 
@@ -475,9 +477,13 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     const double ew = attempt == 0 ? opt_.edge_weight : 1.0;
     if (attempt == 1 && ew == opt_.edge_weight) continue;
     if (attempt == 2 && Hq == opt_.rows_per_wave) break;
+    // 2-D direct: strips that push to a W / E neighbour run longer (their pushes and corner
+    // stores): shorter units for them (opt_.side_weight; 8192x4096 2-D periodic tile, us/step at
+    // weight 1.0 / 1.15 / 1.25 / 1.35 / 1.5: 19.7 / 17.6 / 16.4 / 16.0 / 16.2, alone 14.2)
+    const bool sw = direct_ && (peer[kW] || peer[kNW] || peer[kSW]), se = direct_ && (peer[kE] || peer[kNE] || peer[kSE]);
     UnitPlan Q = plan_units(g, K, Hq, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                             ew, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, hb,
-                            attempt == 0 ? opt_.row_edge_weight : 1.0);
+                            attempt == 0 ? opt_.row_edge_weight : 1.0, opt_.side_weight, G_, sw, se);
     std::map<int, std::pair<int, int>> ends;  // strip -> (top unit, bottom unit) indices
     for (int i = 0; i < (int)Q.interior.size(); ++i) {
       const Unit& u = Q.interior[i];
@@ -1664,6 +1670,13 @@ bool Engine::finalize_convergence(RunStats& st) {
       }
     } else {
       for (Tile& t : tiles_) std::swap(t.keep, t.buf[t.cur]);
+      // the cached exchange descriptors hold the old buffer addresses: rebuild them on next use
+      H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+      H2D_HIP_CHECK(hipStreamSynchronize(comm_));
+      for (auto* m : {&local_descs_, &pack_descs_, &unpack_descs_}) {
+        for (auto& kv : *m) hipFree(std::get<0>(kv.second));
+        m->clear();
+      }
     }
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
     __atomic_store_n(&h_conv_->stop_seq, 0ull, __ATOMIC_RELEASE);

@@ -96,6 +96,8 @@ struct EngineOptions {
   // Strip width of the persistent kernel: 256 (4 columns per lane), 128 (2 per lane: units twice
   // as tall for the same wave count, so a short tile's K-cone costs half as much), 0 auto.
   int pstream_cols = 0;
+  // 2-D direct pipeline: cost weight per row of the units that push to a W / E neighbour
+  double side_weight = 1.35;
   // Diagnostics: per-phase timers of the persistent kernel (PStreamArgs::phase)
   bool phase_timers = false;
   double watchdog_s = 900.0;  // abort the RCCL communicator after this long without progress (0: off)

@@ -73,8 +73,11 @@ struct UnitPlan {
   std::vector<Unit> interior, boundary;
 };
 // row_edge_weight: the cost weight of units whose cone reaches a global edge ROW (<= 0: edge_weight)
+// side_w / side_e: strips whose outputs reach the first / last side_cols columns push them to a
+// W / E neighbour (2-D direct pipeline): their units cost side_weight per row.
 UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
-                    int64_t capacity, const bool* peer, int hb, double row_edge_weight = -1.0);
+                    int64_t capacity, const bool* peer, int hb, double row_edge_weight = -1.0,
+                    double side_weight = 1.0, int side_cols = 0, bool side_w = false, bool side_e = false);
 // Resident waves of the streaming kernel on `device` (occupancy query × CUs × 4 waves/block).
 int64_t stream_wave_capacity(int K, int precision, int device);
 
@@ -220,7 +223,8 @@ struct PStreamArgs {
   unsigned int* timed_out = nullptr;
   unsigned int* timed_out_host = nullptr;
   unsigned long long* wait_acc = nullptr;
-  // Diagnostics (usually null): s_memrealtime ticks (100 MHz) summed over waves and chunks, per
+  // Diagnostics (usually null; recorded only by a build of pstream_kernel.hpp with
+  // -DH2D_PSTREAM_PHASES): s_memrealtime ticks (100 MHz) summed over waves and chunks, per
   // phase of a chunk — [0] chunks, [1] chunk-start drain of the previous chunk's stores, [2]
   // chunk-start wait for the neighbours' rows, [3] halo flag wait, [4] prologue (its loads and
   // the cone rows), [5] steady rows + tail, [6] in-loop waits (the tops' vmcnt + row waits).

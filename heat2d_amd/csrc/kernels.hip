@@ -364,6 +364,7 @@ struct RowRange {
   int64_t strip, a, b;  // rows [a, b) of strip
   bool edge;            // costs `w` per row (global-edge masks)
   bool edge_top = false, edge_bot = false;  // first / last unit is an edge unit (global edge rows)
+  bool side = false;    // costs `side_weight` per row (pushes to a W / E neighbour)
 };
 
 // Cut every range into units of (nearly) equal cost, fitting `capacity` waves in one round.
@@ -371,12 +372,14 @@ struct RowRange {
 // edge unit costs w times more: target cost U -> h = U - K (plain) or U/w - K (edge).
 std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>& strips,
                               const std::vector<RowRange>& ranges, int H, bool fixed, bool per_x, bool per_y,
-                              double edge_weight, int64_t capacity, double row_edge_weight) {
+                              double edge_weight, int64_t capacity, double row_edge_weight, double side_weight = 1.0) {
   // edge units cost more per row: column-edge strips run the column-masked body on every row,
   // row-edge units (their K-cone reaches a global edge row) the row-masked one
   const double w = std::max(1.0, edge_weight);
   const double wr = std::max(1.0, row_edge_weight > 0 ? row_edge_weight : edge_weight);
+  const double ws = std::max(1.0, side_weight);
   auto rows_for = [&](double U, bool edge) { return std::max<int64_t>(1, (int64_t)(edge ? U / w - K : U - K)); };
+  auto rows_side = [&](double U) { return std::max<int64_t>(1, (int64_t)(U / ws - K)); };
   auto rows_row_edge = [&](double U) { return std::max<int64_t>(1, (int64_t)(U / wr - K)); };
   auto plan = [&](double U, std::vector<Unit>* out) -> int64_t {
     int64_t count = 0;
@@ -407,7 +410,7 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
         emit(r.strip, e, b, he);
         b = e;
       }
-      emit(r.strip, a, b, rows_for(U, r.edge));
+      emit(r.strip, a, b, r.side ? rows_side(U) : rows_for(U, r.edge));
     }
     return count;
   };
@@ -418,7 +421,7 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
     // Minimise the estimated makespan ceil(units / capacity) * U: one full round when the
     // tile has few strips (the usual case); several full rounds for huge tiles whose strips
     // alone outnumber the resident waves.  Units never go below 8 rows.
-    const double umin = 8.0 + K, umax = (double)(g.xcell + K) * std::max(w, wr) + 1.0;
+    const double umin = 8.0 + K, umax = (double)(g.xcell + K) * std::max(std::max(w, wr), ws) + 1.0;
     double best_u = umax, best_ms = 1e300;
     // fine steps: with ~60 units per strip a 3 % step left ~3 % of the wave slots empty
     // (4096^2: 993 of 1024 units)
@@ -439,7 +442,8 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
 }  // namespace
 
 UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
-                    int64_t capacity, const bool* peer, int hb, double row_edge_weight) {
+                    int64_t capacity, const bool* peer, int hb, double row_edge_weight, double side_weight,
+                    int side_cols, bool side_w, bool side_e) {
   UnitPlan P;
   const std::vector<Strip> strips = strip_layout(g, K, fixed, per_y);
   const int64_t nstrips = (int64_t)strips.size();
@@ -467,14 +471,16 @@ UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, boo
     if (!has_peer) {
       // units whose K-cone reaches a global edge row are edge units (cost-balanced)
       RowRange r{s, 0, g.xcell, col_edge};
-      r.edge_top = !col_edge && row_edge_top;
-      r.edge_bot = !col_edge && row_edge_bot;
+      r.side = (side_w && S.lo < side_cols) || (side_e && S.hi > g.ycell - side_cols);
+      r.edge_top = !col_edge && !r.side && row_edge_top;
+      r.edge_bot = !col_edge && !r.side && row_edge_bot;
       in_r.push_back(r);
     } else {
       in_r.push_back(RowRange{s, top, bot, col_edge});
     }
   }
-  P.interior = size_ranges(g, K, strips, in_r, H, fixed, per_x, per_y, edge_weight, capacity, row_edge_weight);
+  P.interior = size_ranges(g, K, strips, in_r, H, fixed, per_x, per_y, edge_weight, capacity, row_edge_weight,
+                           side_weight);
   // Boundary units are short (hb rows): they run first, alone, and gate the halo exchange.
   P.boundary = size_ranges(g, K, strips, bd_r, hb, fixed, per_x, per_y, 1.0, capacity, 1.0);
   auto edge_first = [](const Unit& a, const Unit& b) { return (a.flags != 0) > (b.flags != 0); };

@@ -14,7 +14,7 @@
 //
 // Hand-off (MI355X guide, Guideline 16 R1 / visibility table row 1): every output row is
 // stored write-through (buffer_store sc1); a wave publishes "rows complete" in its own progress
-// word with an agent-scope atomic store only after an `s_waitcnt vmcnt(8)` at a steady-loop
+// word with an agent-scope atomic store only after an `s_waitcnt vmcnt(2 RI)` at a steady-loop
 // iteration top — every store issued before the previous top has completed, so the publication
 // lags one iteration and never stalls; consumers poll progress words with relaxed agent loads
 // (one vector load: lane l reads neighbour slot l) and read tile rows with sc1 buffer loads
@@ -113,6 +113,9 @@ __device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int la
 template <int K, bool F32, int EDGE, bool FIXED, int CPL>
 __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w, int lane, PSlot& sl) {
   typedef typename LaneVec<CPL>::T V;
+  // rows per steady iteration (8 for 2-column lanes was measured slower: 512x4096 K=8 2.21 vs
+  // 1.91 us/step — its rows are published an iteration later, so the neighbours start later)
+  constexpr int RI = 4;
   const int h = u.h, n = h + 2 * K;
   const bool rev = (u.flags & kUnitReverse) != 0;
   const bool ns = (u.flags & kUnitNS) != 0;
@@ -166,7 +169,10 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   bool dead = false;         // a wait gave up: finish without waiting (the host reports it)
   bool sig_pending = false;  // a halo unit's pushes of its last chunk are not yet signalled
   double racc = 0.0;
-  // diagnostics: per-phase time of this wave (wave-uniform branch; no cost when a.phase is null)
+  // diagnostics: per-phase time of this wave, compiled in only with -DH2D_PSTREAM_PHASES (even
+  // an untaken runtime branch per iteration top cost ~30 % at 512x4096: the timers' registers
+  // and the loop's scheduling)
+#ifdef H2D_PSTREAM_PHASES
   const bool tm = a.phase != nullptr;
   unsigned long long ph[kPhases] = {};
   unsigned long long tq = tm ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -177,6 +183,9 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       tq = t;
     }
   };
+#else
+  auto lap = [](int) {};
+#endif
   for (int j = 0; j < a.nchunks; ++j) {
     const unsigned cidx = a.cbase + (unsigned)j;
     const int par = (a.cur0 + j) & 1;
@@ -196,7 +205,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       }
       sl.known = max(sl.known, pv);
       lap(1);
-      pensure(sl, 0, min(n, 2 * K + 4), cidx - 1u, a.prog, a, dead);
+      pensure(sl, 0, min(n, 2 * K + RI), cidx - 1u, a.prog, a, dead);
       lap(2);
     }
     const V* hrowp = nullptr;
@@ -242,9 +251,9 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
 #pragma unroll
     for (int i = 0; i < 2 * K; ++i) pro[i] = (i < K && hrowp != nullptr) ? hrowp[(int64_t)i * pitchv]
                                                                         : load_row_sc1<V>(rin, lvoff, soff(i));
-    V pf[4];
+    V pf[RI];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) pf[d] = load_row_sc1<V>(rin, lvoff, soff(min(2 * K + d, n - 1)));
+    for (int d = 0; d < RI; ++d) pf[d] = load_row_sc1<V>(rin, lvoff, soff(min(2 * K + d, n - 1)));
     __builtin_amdgcn_sched_barrier(0);
     prologue<K, F32, EDGE, FIXED, false, true, false, 0>(S, pro, c, k, racc);
     lap(4);
@@ -257,13 +266,14 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
 #define H2D_PSTEADY(D)                                                                \
   {                                                                                   \
     const V nw = pf[D];                                                               \
-    pf[D] = load_row_sc1<V>(rin, lvoff, soff(min(ir0 + (D) + 4, n - 1)));             \
+    pf[D] = load_row_sc1<V>(rin, lvoff, soff(min(ir0 + (D) + RI, n - 1)));            \
     process_row<K, F32, EDGE, FIXED, false, true, false, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
-    for (; ir0 + 4 <= n; ir0 += 4) {
+    for (; ir0 + RI <= n; ir0 += RI) {
       // iteration top: every op before the previous top has completed (>= 8 VMEM ops since)
       lap(5);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if constexpr (RI == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);
       if (pushes && !signalled && issued_prev >= a.sig_rows) {  // the pushed rows have completed
         psignal(a.sig[dir], a.rel, lane);
@@ -273,17 +283,29 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       polled = ppoll(sl, a.prog);  // consumed at the next top
       have_poll = true;
       issued_prev = ir0 - 2 * K;
-      if (j > 0) pensure(sl, ir0 + 4, min(n, ir0 + 8), cidx - 1u, a.prog, a, dead);
+      if (j > 0) pensure(sl, ir0 + RI, min(n, ir0 + 2 * RI), cidx - 1u, a.prog, a, dead);
       lap(6);
       H2D_PSTEADY(0)
       H2D_PSTEADY(1)
       H2D_PSTEADY(2)
       H2D_PSTEADY(3)
+      if constexpr (RI == 8) {
+        H2D_PSTEADY(4)
+        H2D_PSTEADY(5)
+        H2D_PSTEADY(6)
+        H2D_PSTEADY(7)
+      }
     }
 #undef H2D_PSTEADY
     if (ir0 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[0], ir0, c, k, racc);
     if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
     if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
+    if constexpr (RI == 8) {
+      if (ir0 + 3 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 1, K>(S, pf[3], ir0 + 3, c, k, racc);
+      if (ir0 + 4 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[4], ir0 + 4, c, k, racc);
+      if (ir0 + 5 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 1, K>(S, pf[5], ir0 + 5, c, k, racc);
+      if (ir0 + 6 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[6], ir0 + 6, c, k, racc);
+    }
     if (have_poll) sl.known = max(sl.known, polled);
     // pushes not yet signalled at an iteration top: at the next chunk start (or launch end)
     if (pushes && !signalled) sig_pending = true;
@@ -293,11 +315,13 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   ppublish(myprog, (a.cbase + (unsigned)a.nchunks) * (unsigned)h, lane);
   if (sig_pending) psignal(a.sig[dir], a.rel, lane);
   lap(1);
+#ifdef H2D_PSTREAM_PHASES
   if (tm && lane == 0) {
     ph[0] = (unsigned long long)a.nchunks;
 #pragma unroll
     for (int i = 0; i < kPhases; ++i) __hip_atomic_fetch_add(a.phase + i, ph[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#endif
 }
 
 template <int K, bool F32, int CPL>

@@ -465,29 +465,34 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   if (ns_wait || xreads != 0) {
     // wait until the exchange that fills this unit's ghost rows has landed (a wait that already
     // timed out in this engine stops every later wait: fail fast)
-    if (lane == 0 && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+    if (__hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      long long i = 0;
-      // relaxed polls (an acquire per poll is 2-3x slower per hop), ONE acquire after the match
-      if (ns_wait)
-        while (__hip_atomic_load(a.wait[dir], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.need[dir]) {
-          if (++i > a.halo_polls) {
-            report_timeout(a.timed_out, a.timed_out_host, 2u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
+      // every flag this unit needs is polled at once, one per lane (lanes 0-5: the side links,
+      // lane 6: the N/S flag) — one round trip per poll, not one per flag; relaxed polls (an
+      // acquire per poll is 2-3x slower per hop), ONE acquire after the match
+      const unsigned long long* wp = nullptr;
+      unsigned long long wneed = 0;
+#pragma unroll
+      for (int x = 0; x < kSideLinks; ++x)
+        if (lane == x && ((xreads >> x) & 1) != 0) {
+          wp = a.xwait[x];
+          wneed = a.xneed[x];
         }
-      for (int x = 0; x < kSideLinks; ++x) {
-        if (((xreads >> x) & 1) == 0) continue;
-        while (__hip_atomic_load(a.xwait[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.xneed[x]) {
-          if (++i > a.halo_polls) {
-            report_timeout(a.timed_out, a.timed_out_host, 2u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
+      if (lane == kSideLinks && ns_wait) {
+        wp = a.wait[dir];
+        wneed = a.need[dir];
       }
-      if (a.wait_acc != nullptr) {  // exposed halo wait of this unit (fire-and-forget atomics)
+      bool pending = wp != nullptr;
+      for (long long i = 0;; ++i) {
+        if (pending) pending = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < wneed;
+        if (__ballot(pending) == 0ull) break;
+        if (i >= a.halo_polls) {
+          if (lane == 0) report_timeout(a.timed_out, a.timed_out_host, 2u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (a.wait_acc != nullptr && lane == 0) {  // exposed halo wait of this unit (fire-and-forget atomics)
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
         __hip_atomic_fetch_add(a.wait_acc, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add(a.wait_acc + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

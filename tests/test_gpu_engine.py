@@ -456,14 +456,20 @@ def test_fused_convergence_matches_oracle(native, gpu, gx, gy, pipeline):
                                small_grid_lds=False, tiled=0, **PIPELINES[pipeline],
                                **{**CONV, "sensitivity": 0.0})
             first = None
-            for i in range(1, 12):
-                e2.run(9)
-                b2 = _gather(e2, nx, ny) != oracle(native, nx, ny, 9 * i, 1)["grid"]
+            for i in range(1, 40):
+                e2.run(1)
+                g2 = _gather(e2, nx, ny)
+                o2 = oracle(native, nx, ny, i, 1)["grid"]
+                b2 = g2 != o2
                 if b2.any():
                     r2, c2 = np.nonzero(b2)
-                    first = (9 * i, int(b2.sum()), int(r2.min()), int(r2.max()), int(c2.min()), int(c2.max()))
+                    first = (i, int(b2.sum()), int(r2.min()), int(r2.max()), int(c2.min()), int(c2.max()),
+                             float(np.abs(g2 - o2).max()))
+                    rows = sorted(set(r2.tolist()))
+                    print(f"rerun: wrong rows at step {i}: {rows[:40]}", flush=True)
+                    print(f"rerun: tile geoms {[e2.geom(t) for t in range(e2.num_tiles())]}", flush=True)
                     break
-            print(f"rerun: first wrong (steps, cells, rows, cols) {first}", flush=True)
+            print(f"rerun: first wrong (steps, cells, rows, cols, max|d|) {first}", flush=True)
 
             def ranges(v):
                 v = sorted(set(int(x) for x in v))

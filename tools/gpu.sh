@@ -45,6 +45,8 @@ for s in "$@"; do
     pphases) step pphases 300 python -u tools/pstream_check.py phases ;;
     profconv) step profconv 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profconv -o run -- python tools/conv_probe.py 80x64 ;;
     stress) step stress 400 python -u tools/stress_flaky.py 30 ;;
+    sideweight) step sideweight 400 python -u tools/timeline.py 8192x4096:7:70 8192x4096:7:70:direct2d:side_weight=1.0 8192x4096:7:70:direct2d:side_weight=1.15 8192x4096:7:70:direct2d:side_weight=1.25 8192x4096:7:70:direct2d:side_weight=1.35 8192x4096:7:70:direct2d:side_weight=1.5 --json gpurun_out/sideweight.json ;;
+    stressseq) step stressseq 400 python -u tools/stress_seq.py 12 ;;
     pksweep) step pksweep 300 python -u tools/pstream_check.py ksweep ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;

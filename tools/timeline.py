@@ -57,7 +57,7 @@ def run_case(n, spec):
     kw = dict(tblock=K, device=0, small_grid_lds=False, tiled=0, timeline=64)
     for extra in parts[4:]:  # engine options, name=value (e.g. direct_acquire=2)
         name, value = extra.split("=")
-        kw[name] = int(value)
+        kw[name] = float(value) if "." in value else int(value)
     if direct:
         # direct2d: periodic in both dimensions — all eight neighbours are the tile itself (the
         # per-rank shape of a 2-D block decomposition)
