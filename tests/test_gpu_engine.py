@@ -570,3 +570,54 @@ def test_fused_convergence_rccl_and_ipc_self(native, gpu):
     st = eng.run(5000)
     assert st["converged"] and st["steps_done"] == ref["steps_done"] == 219
     assert np.array_equal(eng.download(0), ref["grid"])
+
+
+# ---- persistent pipelined stencil (pstream_kernel.hpp) -------------------------------------
+@pytest.mark.parametrize("cols", [256, 128])
+@pytest.mark.parametrize("nx,ny,K,steps,boundary", [(300, 517, 7, 37, 0), (257, 1000, 4, 41, 1), (203, 611, 1, 5, 0),
+                                                    (203, 611, 3, 9, 1), (512, 4096, 8, 40, 0), (96, 300, 5, 26, 1)])
+def test_persistent_kernel_bitexact(native, gpu, cols, nx, ny, K, steps, boundary):
+    """Runs of equal chunks in ONE persistent launch (forced on a lone tile), both strip widths,
+    NaN-poisoned ghost ring: bit-exact with the oracle, and a second run continues the progress
+    words of the same plan."""
+    e = native.Engine(nx, ny, tblock=K, device=gpu, small_grid_lds=False, tiled=0, persistent=1, pstream_cols=cols,
+                      boundary=boundary, poison=True, halo_timeout_s=5.0)
+    assert e.pstream_units(K), "no persistent plan"
+    e.run(steps)
+    assert e.pstream_launches() >= 1
+    assert np.array_equal(e.download(0), oracle(native, nx, ny, steps, boundary)["grid"])
+    e.run(steps)
+    assert np.array_equal(e.download(0), oracle(native, nx, ny, 2 * steps, boundary)["grid"])
+
+
+@pytest.mark.parametrize("rows,K,cols", [(512, 8, 128), (512, 8, 256), (1024, 8, 256), (300, 6, 128)])
+def test_persistent_direct_row_periodic(native, gpu, rows, K, cols):
+    """The per-rank shape of strong scaling through the direct pipeline with the persistent
+    kernel (the auto choice for short strips): bit-exact, halo waits counted, and the chunk
+    sequence continues across runs and across a convergence-free re-run."""
+    steps = 5 * K + 3
+    e = native.Engine(rows, 4096, periodic_x=True, tblock=K, device=gpu, ranks=[0], transport=native.TRANSPORT_IPC,
+                      halo_timeout_s=5.0, pstream_cols=cols)
+    e.ipc_open([e.ipc_handle()])
+    e.ipc_prime()
+    e.reset_halo_wait()
+    e.run(steps)
+    assert e.pstream_launches() >= 1
+    assert np.array_equal(e.download(0), oracle(native, rows, 4096, steps, per=(True, False))["grid"])
+    assert e.halo_wait()["waits"] > 0
+    e.run(2 * K)
+    assert np.array_equal(e.download(0), oracle(native, rows, 4096, steps + 2 * K, per=(True, False))["grid"])
+
+
+def test_persistent_auto_policy(native, gpu):
+    """Auto: the persistent kernel only for the direct pipeline's short strips, never for a lone
+    tile (there launch per chunk is faster)."""
+    e = native.Engine(512, 4096, tblock=8, device=gpu, small_grid_lds=False, tiled=0)
+    e.run(40)
+    assert e.pstream_launches() == 0
+    d = native.Engine(512, 4096, periodic_x=True, tblock=8, device=gpu, ranks=[0], transport=native.TRANSPORT_IPC,
+                      halo_timeout_s=5.0)
+    d.ipc_open([d.ipc_handle()])
+    d.ipc_prime()
+    d.run(40)
+    assert d.pstream_launches() >= 1
