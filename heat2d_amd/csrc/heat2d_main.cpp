@@ -325,6 +325,8 @@ int main(int argc, char** argv) {
   const std::string tsel = a.count("transport") ? a["transport"] : "auto";
   if (world > 1) {
     o.ranks = {env.rank};
+    // ranks sharing a GPU: no persistent launches (each needs every one of its waves resident)
+    if (world > std::max(1, ndev)) o.persistent = 0;
     if (dev != "gpu") o.transport = kTransportExternal;
     // direct IPC needs halo units of at least max(K, G) rows at both ends of every strip (and,
     // for 2-D blocks, tiles 4-column aligned: the engine refuses others and every rank falls

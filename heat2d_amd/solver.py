@@ -203,6 +203,10 @@ class Solver:
         if cfg.pipeline not in PIPELINE_OPTIONS:
             raise ValueError(f"unknown pipeline {cfg.pipeline!r}")
         kw.update(PIPELINE_OPTIONS[cfg.pipeline])
+        if self.device >= 0 and self.ctx.world > max(1, n.device_count()):
+            # ranks share a GPU: a persistent launch needs every one of its waves resident, which
+            # another rank's persistent launch on the same GPU could prevent — launch per chunk
+            kw["persistent"] = 0
         kw.update(getattr(self, "engine_kw", {}))
         return n.Engine(
             cfg.nx, cfg.ny, gridx=self.gridx, gridy=self.gridy, periodic_x=self.model.periodic_x,
