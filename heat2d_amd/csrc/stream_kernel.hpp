@@ -311,6 +311,25 @@ __device__ __forceinline__ void prologue(V (&S)[K][2], const V (&pro)[2 * K], co
   }
 }
 
+// Prologue rows loaded where they are used (H2D_PRO_UPFRONT=0, the default) or all up front
+// (=1).  A/B at 4096^2, depth 7, alternating processes (tools/ab_so.py, profiles/ab_prologue_r3.txt):
+// us/step 1000 steps 7.67/7.84/7.79 inline vs 7.79/7.78/7.94 up front; 20 steps 8.36/8.44/8.52 vs
+// 8.41/8.53/8.64.
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int IR>
+__device__ __forceinline__ void prologue_inline(float4 (&S)[K][2], const float4* __restrict__ rowp,
+                                                const float4* __restrict__ hrowp, int64_t pitch4, const LaneCtx& c,
+                                                const Coef& k, double& racc) {
+  if constexpr (IR < 2 * K) {
+    const float4 v = (IR < K ? hrowp : rowp)[(int64_t)IR * pitch4];
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR & 1, IR / 2>(S, v, IR, c, k, racc);
+    prologue_inline<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR + 1>(S, rowp, hrowp, pitch4, c, k, racc);
+  }
+}
+
+#ifndef H2D_PRO_UPFRONT
+#define H2D_PRO_UPFRONT 0
+#endif
+
 // Mid-unit signal of the signalled halo pipeline: this wave's halo rows are stored — release
 // them at system scope and count the unit.  Producer recipe of the MI355X guide: the wave's
 // stores drained, the release fence (L2 write-back), an explicit drain again (ROCm 7.2 can
@@ -345,6 +364,7 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
   // vmcnt(0) — several serialised round trips, ~3 us of every launch).  Stream rows [0, K) are
   // the unit's outer cone rows: for a halo unit, the ghost rows, read from hrowp (the halo
   // receive buffer of the direct pipeline; == rowp otherwise).
+#if H2D_PRO_UPFRONT
   float4 pro[2 * K];
 #pragma unroll
   for (int i = 0; i < 2 * K; ++i) pro[i] = (i < K ? hrowp : rowp)[(int64_t)i * pitch4];
@@ -353,6 +373,12 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
   for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(2 * K + d, n - 1) * pitch4];
   __builtin_amdgcn_sched_barrier(0);  // keep the loads above: each use waits only for its own row
   prologue<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0>(S, pro, c, k, racc);
+#else
+  float4 pf[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(2 * K + d, n - 1) * pitch4];
+  prologue_inline<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0>(S, rowp, hrowp, pitch4, c, k, racc);
+#endif
 
   int ir0 = 2 * K;  // even: slot parity of sub-step d is d & 1
 #define H2D_STEADY(D)                                                        \
