@@ -47,6 +47,7 @@ for s in "$@"; do
     stress) step stress 400 python -u tools/stress_flaky.py 30 ;;
     sideweight) step sideweight 400 python -u tools/timeline.py 8192x4096:7:70 8192x4096:7:70:direct2d:side_weight=1.0 8192x4096:7:70:direct2d:side_weight=1.15 8192x4096:7:70:direct2d:side_weight=1.25 8192x4096:7:70:direct2d:side_weight=1.35 8192x4096:7:70:direct2d:side_weight=1.5 --json gpurun_out/sideweight.json ;;
     stressseq) step stressseq 400 python -u tools/stress_seq.py 12 ;;
+    pmcpst) step pmcpst 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_VALU --kernel-trace --stats -d gpurun_out/pmcpst -o run -- python tools/prof_pstream.py 512 128 ;;
     pksweep) step pksweep 300 python -u tools/pstream_check.py ksweep ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;
