@@ -179,3 +179,18 @@ def test_native_cli_ranks_ipc_on_gpu(native, gpu, tmp_path, n, gx, conv):
     assert '"pipeline": "direct"' in r.stdout and f'"ranks": {n}' in r.stdout
     ref = native.oracle_run(nx, ny, steps, **kw)["grid"]
     assert np.array_equal(read_grid(tmp_path / "final_binary.dat", nx, ny), ref)
+
+
+def test_gpu_halo_wait_sees_a_late_neighbour(tmp_path):
+    """The exposed halo wait (the MPI_Waitall analogue, Report.pdf p.34-37): a neighbour that
+    starts 50 ms late shows up in the waiting rank's in-kernel halo-wait counters, not in the
+    late rank's."""
+    out = _torchrun(2, [os.path.join(ROOT, "tests", "_halo_delay_worker.py")], str(tmp_path))
+    # the two ranks' lines can interleave on the launcher's stdout: pick the JSON objects out
+    import re
+
+    recs = {d["rank"]: d for d in (json.loads(m) for m in re.findall(r'\{"rank"[^{}]*\}', out))}
+    assert set(recs) == {0, 1}
+    assert recs[0]["max_us"] > 20000.0, recs
+    assert recs[1]["max_us"] < recs[0]["max_us"], recs
+    assert recs[0]["waits"] > 0 and recs[1]["waits"] > 0
