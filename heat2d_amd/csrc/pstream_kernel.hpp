@@ -116,6 +116,14 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   // rows per steady iteration (8 for 2-column lanes was measured slower: 512x4096 K=8 2.21 vs
   // 1.91 us/step — its rows are published an iteration later, so the neighbours start later)
   constexpr int RI = 4;
+  // publish (drain to the iteration before, store the progress word, poll the neighbours) at
+  // every PE-th iteration top of a 2-column lane (H2D_PSTREAM_PE2).  Measured: every 2nd top is
+  // slower (512x4096 K=8 2.21 vs 1.93 us/step) although it halves the drains — fresh progress
+  // words matter more to the neighbours than the exposed store latency costs this wave.
+#ifndef H2D_PSTREAM_PE2
+#define H2D_PSTREAM_PE2 1
+#endif
+  constexpr int PE = CPL == 2 ? H2D_PSTREAM_PE2 : 1;
   const int h = u.h, n = h + 2 * K;
   const bool rev = (u.flags & kUnitReverse) != 0;
   const bool ns = (u.flags & kUnitNS) != 0;
@@ -269,19 +277,22 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
     pf[D] = load_row_sc1<V>(rin, lvoff, soff(min(ir0 + (D) + RI, n - 1)));            \
     process_row<K, F32, EDGE, FIXED, false, true, false, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
+    int it = 0;
     for (; ir0 + RI <= n; ir0 += RI) {
-      // iteration top: every op before the previous top has completed (>= 8 VMEM ops since)
       lap(5);
-      if constexpr (RI == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);
-      if (pushes && !signalled && issued_prev >= a.sig_rows) {  // the pushed rows have completed
-        psignal(a.sig[dir], a.rel, lane);
-        signalled = true;
+      if (PE == 1 || (it++ % PE) == 0) {
+        // publishing top: every op before the previous top has completed (>= 8 VMEM ops since)
+        if constexpr (RI == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);
+        if (pushes && !signalled && issued_prev >= a.sig_rows) {  // the pushed rows have completed
+          psignal(a.sig[dir], a.rel, lane);
+          signalled = true;
+        }
+        if (have_poll) sl.known = max(sl.known, polled);
+        polled = ppoll(sl, a.prog);  // consumed at the next publishing top
+        have_poll = true;
       }
-      if (have_poll) sl.known = max(sl.known, polled);
-      polled = ppoll(sl, a.prog);  // consumed at the next top
-      have_poll = true;
       issued_prev = ir0 - 2 * K;
       if (j > 0) pensure(sl, ir0 + RI, min(n, ir0 + 2 * RI), cidx - 1u, a.prog, a, dead);
       lap(6);

@@ -25,10 +25,6 @@ for s in "$@"; do
   case "$s" in
     tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     tests-nox) step tests-nox 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
-    diagconv2) step diagconv2 300 python -u tools/diag_conv2.py ;;
-    diagconv2b) HIP_LAUNCH_BLOCKING=1 step diagconv2b 300 python -u tools/diag_conv2.py ;;
-    diagstale) step diagstale 300 python -u tools/diag_stale.py ;;
-    diagconv) step diagconv 300 python -u tools/diag_conv.py ;;
     engine-file) step engine-file 600 python -u -m pytest tests/test_gpu_engine.py -q --timeout 300 --timeout-method thread -rf ;;
     tests-k) step tests-k 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf -k "$TESTK" ;;
     tests-new) step tests-new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
@@ -57,9 +53,6 @@ for s in "$@"; do
                 --json gpurun_out/timeline.json ;;
     timeline2) step timeline2 300 python -u tools/timeline.py 512x4096:6:60 512x4096:6:60:direct 1024x4096:7:70 \
                  8192x4096:7:70 8192x4096:7:70:direct2d 4096x4096:7:70 --json gpurun_out/timeline2.json ;;
-    diag2d) step diag2d 400 python -u tools/diag2d.py 257 4096 5 3 ;;
-    diag2db) step diag2db 400 python -u tools/diag2d.py 257 4096 5 2 fp ;;
-    diag2dc) step diag2dc 400 python -u tools/diag2d.py 96 300 5 1 f ;;
     proxy) step proxy 600 python -u tools/strong_proxy.py 4096 840 6,7,8 0 '' 1,2,4,8 ;;
     prof) step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
             python bench.py --steps 20 --warmup 5 --repeat 3 ;;
