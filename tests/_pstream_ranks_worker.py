@@ -1,0 +1,38 @@
+"""Worker of test_gpu_persistent_two_processes (torch.distributed.run, 2 ranks on one GPU): row
+strips through the direct IPC pipeline with the persistent kernel on both ranks (small tiles, so
+both launches' waves fit on the GPU together); every rank's tile is compared with the oracle."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from heat2d_amd._native import native  # noqa: E402
+
+n = native()
+dist.init_process_group("gloo")
+rank = dist.get_rank()
+nx, ny, K, steps = 2 * 192 + 1, 2048, 8, 5 * 8 + 3
+e = n.Engine(nx, ny, gridx=2, gridy=1, tblock=K, device=0, ranks=[rank], transport=n.TRANSPORT_IPC,
+             halo_timeout_s=10.0, persistent=1, pstream_cols=128)
+hs = [None, None]
+dist.all_gather_object(hs, e.ipc_handle())
+e.ipc_open(hs)
+dist.barrier()
+e.ipc_prime()
+dist.barrier()
+e.run(steps)
+e.synchronize()
+g = e.geom(0)
+ref = n.oracle_run(nx, ny, steps)["grid"][g["gx0"]:g["gx0"] + g["xcell"], :]
+ok = bool(np.array_equal(e.download(0), ref))
+dist.barrier()
+e.run(2 * K)
+e.synchronize()
+ref2 = n.oracle_run(nx, ny, steps + 2 * K)["grid"][g["gx0"]:g["gx0"] + g["xcell"], :]
+ok2 = bool(np.array_equal(e.download(0), ref2))
+print(json.dumps({"rank": rank, "ok": ok, "ok2": ok2, "launches": e.pstream_launches()}), flush=True)
+dist.barrier()
+dist.destroy_process_group()

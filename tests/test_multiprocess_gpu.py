@@ -194,3 +194,15 @@ def test_gpu_halo_wait_sees_a_late_neighbour(tmp_path):
     assert recs[0]["max_us"] > 20000.0, recs
     assert recs[1]["max_us"] < recs[0]["max_us"], recs
     assert recs[0]["waits"] > 0 and recs[1]["waits"] > 0
+
+
+def test_gpu_persistent_two_processes(tmp_path):
+    """The persistent kernel on two ranks of the direct pipeline (separate processes, IPC handles
+    carrying each rank's persistent push counts): bit-exact on both ranks, across two runs."""
+    import re
+
+    out = _torchrun(2, [os.path.join(ROOT, "tests", "_pstream_ranks_worker.py")], str(tmp_path))
+    recs = {d["rank"]: d for d in (json.loads(m) for m in re.findall(r'\{"rank"[^{}]*\}', out))}
+    assert set(recs) == {0, 1}, out[-2000:]
+    for r in recs.values():
+        assert r["ok"] and r["ok2"] and r["launches"] >= 1, recs
