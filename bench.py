@@ -91,6 +91,9 @@ def main() -> int:
                          "236/194/180 us for its three 20-step runs (steady: ~171 us)")
     ap.add_argument("--sync-mode", type=int, default=2, choices=(0, 1, 2, 3),
                     help="engine end-of-run synchronisation (EngineOptions::sync_mode)")
+    ap.add_argument("--persistent", choices=("auto", "on", "off"), default="auto",
+                    help="persistent stencil launches (auto: the engine's policy, off when ranks share a GPU; "
+                         "on: also then — a rehearsal whose ranks' plans fit the GPU together)")
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: rehearsal of the distributed contract on the host (gloo), not a benchmark")
     a = ap.parse_args()
@@ -116,7 +119,8 @@ def main() -> int:
     if on_gpu and ndev == 0:
         raise SystemExit("bench: no HIP device (use --device cpu for a host rehearsal)")
     device = (ctx.local_rank % ndev) if on_gpu else -1
-    ctx.distinct_devices = on_gpu and world <= ndev
+    # one physical GPU per rank? (collective; host + PCI bus id, whatever the visibility setup)
+    ctx.devices_shared(device, n.device_pci_id(device) if on_gpu else "")
     if on_gpu:
         torch.cuda.set_device(device)
     bnd = 0 if a.boundary == "fixed" else 1
@@ -146,7 +150,7 @@ def main() -> int:
         c = Config(preset="heat2d", nx=nx_, ny=ny_, steps=steps_, gridx=gridx, gridy=gridy, boundary=a.boundary,
                    precision=a.precision, init="exact", output="none", device=a.device, transport=transport,
                    tblock=a.tblock, rows_per_wave=a.rows_per_wave, overlap=not a.no_overlap, pipeline=pipeline,
-                   quiet=True, report="grad", text_style="grad", sync_mode=a.sync_mode)
+                   quiet=True, report="grad", text_style="grad", sync_mode=a.sync_mode, persistent=a.persistent)
         if conv:  # checks every G+1 steps that never converge (gate only)
             c.convergence, c.interval, c.sensitivity = True, a.tblock + 1, 0.0
         return c

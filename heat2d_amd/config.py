@@ -48,6 +48,7 @@ class Config:
     overlap: bool = True
     pipeline: str = "auto"  # auto | direct-sys | signal | serial (multi-rank halo pipeline)
     sync_mode: int = 0  # end-of-run synchronisation (EngineOptions::sync_mode; the bench uses 2)
+    persistent: str = "auto"  # auto | on | off: persistent stencil launches (auto: off when ranks share a GPU)
     halo_timeout_s: float = 30.0  # bounded device-side halo waits give up (and the run fails) after this
     small_grid: bool = True
     tiled: str = "auto"  # auto | on | off: LDS-tiled temporally-blocked kernel (single-tile small/medium grids)

@@ -6,6 +6,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -179,6 +180,9 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     }
     d_wait_acc_ = dmalloc<unsigned long long>(4);
     dzero(d_wait_acc_, 4 * sizeof(unsigned long long));
+    d_lid_seen_ = dmalloc<unsigned long long>(2);
+    dzero(d_lid_seen_, 2 * sizeof(unsigned long long));
+    d_copies_done_ = d_lid_seen_ + 1;
     if (o.timeline > 0) {
       if (o.timeline > 4096) throw std::invalid_argument("timeline: at most 4096 launches");
       d_stamps_ = dmalloc<unsigned long long>((size_t)o.timeline * kTimelineUnits * 4);
@@ -346,7 +350,7 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
 Engine::~Engine() {
   if (rccl_comm_) ncclCommDestroy((ncclComm_t)rccl_comm_);
   if (!on_gpu()) {
-    for (auto& kv : local_descs_) delete[] std::get<0>(kv.second);
+    for (auto& kv : local_descs_) delete[] kv.second.d;
     return;
   }
   hipDeviceSynchronize();
@@ -377,8 +381,9 @@ Engine::~Engine() {
   if (h_timeout_) hipHostFree(h_timeout_);
   hipFree(halo_counter_);
   for (auto* m : {&local_descs_, &pack_descs_, &unpack_descs_})
-    for (auto& kv : *m) hipFree(std::get<0>(kv.second));
+    for (auto& kv : *m) hipFree(kv.second.d);
   for (auto& t : tiles_) hipFree(t.partials);
+  hipFree(d_lid_seen_);
   hipFree(d_resid_);
   hipHostFree(h_resid_);
   hipFree(d_lds_steps_);
@@ -556,6 +561,11 @@ const Engine::UnitLists& Engine::units(int t, int K) {
   std::vector<Unit> all = in;
   all.insert(all.end(), bd.begin(), bd.end());
   if (all.size() > (size_t)(1 << 30)) throw std::runtime_error("too many work units");
+  // integrity tags: every list its own (process-wide), carried by each of its units
+  for (int i = 0; i < 4; ++i) L.tag[i] = next_tag();
+  for (Unit& u : all) u.tag = L.tag[0];
+  for (Unit& u : in) u.tag = L.tag[1];
+  for (Unit& u : bd) u.tag = L.tag[2];
   L.H = 0;
   for (const Unit& u : in) L.H = std::max(L.H, u.h);
   for (const Unit& u : bd) {
@@ -579,6 +589,7 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     if (!bd.empty()) h2d(L.d_boundary, bd.data(), bd.size() * sizeof(Unit));
     std::vector<Unit> bfirst = bd;
     bfirst.insert(bfirst.end(), in.begin(), in.end());
+    for (Unit& u : bfirst) u.tag = L.tag[3];
     L.d_bfirst = dmalloc<Unit>(bfirst.size());
     h2d(L.d_bfirst, bfirst.data(), bfirst.size() * sizeof(Unit));
     Tile& tw = tiles_[t];
@@ -631,6 +642,17 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     a.stop = d_stop_;
     // the rollback copy: a lone tile recomputes it on convergence instead (no 4 B/cell write per check)
     if (residual && !recompute_rollback()) a.keep = tl.keep;
+  }
+  // integrity: launch id at both ends of the arguments, the list's tag, the device error word
+  a.lid = a.lid_tail = ++lid_;
+  a.utag = L.tag[which];
+  a.lid_seen = d_lid_seen_;
+  a.timed_out = d_sig_timeout_;
+  a.timed_out_host = h_timeout_dev_;
+  if (transport_ == kTransportLocal && has_exchange_ && sig_mode_ == 0 && (stream == nullptr || stream == compute_)) {
+    // serial local pipeline: the exchange copies in front of this launch on the compute stream
+    a.copies_done = d_copies_done_;
+    a.copies_need = copies_need_;
   }
   if (which == 0) {
     a.units = L.d_all;
@@ -770,14 +792,41 @@ int Engine::next_chunk(int64_t done, int64_t total, bool* check) const {
   return (int)k;
 }
 
-CopyDesc* Engine::local_descs(int K, int& n, int64_t& maxe) {
+int Engine::next_tag() {
+  static std::atomic<int> seq{0};
+  int t = 0;
+  while (t == 0) t = (int)((unsigned)seq.fetch_add(1) * 2654435761u);  // spread, never 0
+  return t;
+}
+
+Engine::DescList Engine::upload_descs(std::vector<CopyDesc>& v) {
+  DescList L;
+  L.n = (int)v.size();
+  L.tag = next_tag();
+  for (CopyDesc& c : v) {
+    c.tag = L.tag;
+    L.maxe = std::max(L.maxe, c.rows * c.cols);
+  }
+  if (on_gpu()) {
+    if (!v.empty()) {
+      L.d = dmalloc<CopyDesc>(v.size());
+      h2d(L.d, v.data(), v.size() * sizeof(CopyDesc));
+    }
+  } else {
+    // CPU: keep the host descriptors alive in a heap block
+    L.d = new CopyDesc[v.size() ? v.size() : 1];
+    std::copy(v.begin(), v.end(), L.d);
+  }
+  return L;
+}
+
+const Engine::DescList& Engine::local_descs(int K) {
   // Tile-to-tile copies: peer's owned edge (its current buffer) -> my ghost ring.
   const int parity = tiles_[0].cur;
   auto key = std::make_pair(K, parity);
   auto it = local_descs_.find(key);
   if (it == local_descs_.end()) {
     std::vector<CopyDesc> v;
-    int64_t me = 0;
     std::map<int, int> tile_of_rank;
     for (int t = 0; t < (int)tiles_.size(); ++t) tile_of_rank[tiles_[t].rank] = t;
     for (int t = 0; t < (int)tiles_.size(); ++t) {
@@ -792,35 +841,29 @@ CopyDesc* Engine::local_descs(int K, int& n, int64_t& maxe) {
         if (s.rows != r.rows || s.cols != r.cols) throw std::logic_error("halo shape mismatch");
         v.push_back(CopyDesc{U.buf[U.cur] + U.g.idx(s.r0, s.c0), T.buf[T.cur] + T.g.idx(r.r0, r.c0), U.g.pitch,
                              T.g.pitch, r.rows, r.cols});
-        me = std::max(me, r.count());
       }
     }
-    CopyDesc* dd = nullptr;
-    if (on_gpu() && !v.empty()) {
-      dd = dmalloc<CopyDesc>(v.size());
-      h2d(dd, v.data(), v.size() * sizeof(CopyDesc));
-    } else if (!on_gpu()) {
-      // CPU: keep the host descriptors alive in a heap block.
-      dd = new CopyDesc[v.size() ? v.size() : 1];
-      std::copy(v.begin(), v.end(), dd);
-    }
-    it = local_descs_.emplace(key, std::make_tuple(dd, (int)v.size(), me)).first;
+    it = local_descs_.emplace(key, upload_descs(v)).first;
   }
-  n = std::get<1>(it->second);
-  maxe = std::get<2>(it->second);
-  return std::get<0>(it->second);
+  return it->second;
+}
+
+void Engine::local_copy(const DescList& D, hipStream_t s) {
+  // on the compute stream the copy blocks are counted: the serial pipeline's stencil launch
+  // checks that all of them completed before it started (kIntegOrder)
+  const bool counted = s == compute_;
+  launch_copy_rects(D.d, D.n, D.maxe, s, D.tag, counted ? d_copies_done_ : nullptr, d_sig_timeout_, h_timeout_dev_);
+  if (counted) copies_need_ += (unsigned long long)copy_rects_blocks(D.n, D.maxe);
 }
 
 void Engine::exchange_local(int k) {
   if (!has_exchange_) return;
-  int n = 0;
-  int64_t me = 0;
-  CopyDesc* d = local_descs(k, n, me);
-  if (n == 0) return;
+  const DescList& D = local_descs(k);
+  if (D.n == 0) return;
   if (on_gpu()) {
-    launch_copy_rects(d, n, me, compute_);
+    local_copy(D, compute_);
   } else {
-    cpu_copy_rects(std::vector<CopyDesc>(d, d + n));
+    cpu_copy_rects(std::vector<CopyDesc>(D.d, D.d + D.n));
   }
 }
 
@@ -828,10 +871,7 @@ void Engine::do_exchange_async(int K, hipStream_t s) {
   // Runs on comm_ after ev_ready_ (or, serial pipeline, in order on the compute stream).
   hipStream_t xs = s ? s : comm_;
   if (transport_ == kTransportLocal) {
-    int n = 0;
-    int64_t me = 0;
-    CopyDesc* d = local_descs(K, n, me);
-    launch_copy_rects(d, n, me, xs);
+    local_copy(local_descs(K), xs);
     return;
   }
   if (transport_ != kTransportRccl) throw std::logic_error("do_exchange_async: transport");
@@ -871,7 +911,7 @@ void Engine::do_exchange_async(int K, hipStream_t s) {
     d_send_ = dmalloc<float>((size_t)stage_cap_);
     d_recv_ = dmalloc<float>((size_t)stage_cap_);
     for (auto* m : {&pack_descs_, &unpack_descs_}) {
-      for (auto& kv : *m) hipFree(std::get<0>(kv.second));
+      for (auto& kv : *m) hipFree(kv.second.d);
       m->clear();
     }
   }
@@ -881,17 +921,13 @@ void Engine::do_exchange_async(int K, hipStream_t s) {
     std::vector<CopyDesc> pv, uv;
     plan_pack_descs(p, T.g, T.buf[T.cur], d_send_, pv);
     plan_unpack_descs(p, T.g, T.buf[T.cur], d_recv_, uv);
-    int64_t me = 0;
-    for (auto& c : pv) me = std::max(me, c.rows * c.cols);
-    CopyDesc* dp = dmalloc<CopyDesc>(pv.size());
-    CopyDesc* du = dmalloc<CopyDesc>(uv.size());
-    if (!pv.empty()) h2d(dp, pv.data(), pv.size() * sizeof(CopyDesc));
-    if (!uv.empty()) h2d(du, uv.data(), uv.size() * sizeof(CopyDesc));
-    ip = pack_descs_.emplace(key, std::make_tuple(dp, (int)pv.size(), me)).first;
-    unpack_descs_.emplace(key, std::make_tuple(du, (int)uv.size(), me));
+    DescList dp = upload_descs(pv), du = upload_descs(uv);
+    ip = pack_descs_.emplace(key, dp).first;
+    unpack_descs_.emplace(key, du);
   }
   auto iu = unpack_descs_.find(key);
-  launch_copy_rects(std::get<0>(ip->second), std::get<1>(ip->second), std::get<2>(ip->second), xs);
+  const DescList& P = ip->second;
+  launch_copy_rects(P.d, P.n, P.maxe, xs, P.tag, nullptr, d_sig_timeout_, h_timeout_dev_);
   H2D_NCCL_CHECK(ncclGroupStart());
   // Send segment d to peer[d]; receive the peer's matching segment into ghost side opp(d)
   // from peer[opp(d)].  Posting both in direction order keeps per-peer FIFO matching
@@ -906,7 +942,8 @@ void Engine::do_exchange_async(int K, hipStream_t s) {
     H2D_NCCL_CHECK(ncclRecv(d_recv_ + p.recv_off[g], (size_t)p.recv_rect[g].count(), ncclFloat, p.peer[g], comm, xs));
   }
   H2D_NCCL_CHECK(ncclGroupEnd());
-  launch_copy_rects(std::get<0>(iu->second), std::get<1>(iu->second), std::get<2>(iu->second), xs);
+  const DescList& U = iu->second;
+  launch_copy_rects(U.d, U.n, U.maxe, xs, U.tag, nullptr, d_sig_timeout_, h_timeout_dev_);
 }
 
 void Engine::gate_exchange() {
@@ -1066,12 +1103,27 @@ void Engine::poll_abort() {
   // host's sig/halo sequence numbers no longer match the device counters, so this engine
   // cannot be reused.  Drain what is queued (bounded waits: it terminates).
   broken_ = true;
-  broken_why_ = std::string("signalled halo pipeline timed out: ") +
-                ((to & 1) ? "the exchange gate (boundary units never completed) " : "") +
-                ((to & 2) ? "the device-side halo wait (the exchange never landed) " : "") +
-                ((to & 4) ? "the residual all-reduce (a rank never contributed)" : "");
   hipStreamSynchronize(comm_);
   hipStreamSynchronize(compute_);
+  // the host mirror holds the latest bit; the device word all of them
+  unsigned int all = to;
+  if (hipMemcpy(&all, d_sig_timeout_, sizeof(all), hipMemcpyDeviceToHost) != hipSuccess) all = to;
+  all |= to;
+  const unsigned integ = kIntegArgs | kIntegUnits | kIntegReplay | kIntegDescs | kIntegOrder;
+  if (all & integ) {
+    broken_why_ = std::string("integrity check failed (bits ") + std::to_string(all) + "): " +
+                  ((all & kIntegArgs) ? "torn kernel arguments (launch ids at the two ends differ) " : "") +
+                  ((all & kIntegUnits) ? "a work unit of another list (stale unit-list upload) " : "") +
+                  ((all & kIntegReplay) ? "a launch ran with the arguments of an earlier launch " : "") +
+                  ((all & kIntegDescs) ? "a copy descriptor of another list (stale descriptor upload) " : "") +
+                  ((all & kIntegOrder) ? "a stencil launch started before its exchange copy finished " : "");
+  } else {
+    broken_why_ = std::string("signalled halo pipeline timed out: ") +
+                  ((all & 1) ? "the exchange gate (boundary units never completed) " : "") +
+                  ((all & 2) ? "the device-side halo wait (the exchange never landed) " : "") +
+                  ((all & 4) ? "the residual all-reduce (a rank never contributed) " : "") +
+                  ((all & 8) ? "the persistent kernel's neighbour wait" : "");
+  }
   throw std::runtime_error(broken_why_);
 }
 
@@ -1463,8 +1515,9 @@ const Engine::PPlan* Engine::pplan(int K) {
   // 4096^2 7.744 vs 9.207 — profiles/pstream_r3.txt).  Timeline runs stamp per-chunk launches.
   const bool want = opt_.persistent > 0 ||
                     (opt_.persistent < 0 && direct_ && has_exchange_ && g.xcell <= 1536 && opt_.timeline == 0 && K >= 2);
+  // (every wave must be resident: not with CUs reserved for the comm stream)
   const bool ok_path = on_gpu() && !opt_.naive && !tiled_ && want && tiles_.size() == 1 && K <= kMaxPK && K <= G_ &&
-                       stream_k_supported(K) && !fused_;
+                       stream_k_supported(K) && !fused_ && comm_cus_ == 0;
   bool halo_n = false, halo_s = false, ok = ok_path;
   if (ok && has_exchange_) {
     // only the direct pipeline of 1-D row strips (no west / east / corner neighbours)
@@ -1674,7 +1727,7 @@ bool Engine::finalize_convergence(RunStats& st) {
       H2D_HIP_CHECK(hipStreamSynchronize(compute_));
       H2D_HIP_CHECK(hipStreamSynchronize(comm_));
       for (auto* m : {&local_descs_, &pack_descs_, &unpack_descs_}) {
-        for (auto& kv : *m) hipFree(std::get<0>(kv.second));
+        for (auto& kv : *m) hipFree(kv.second.d);
         m->clear();
       }
     }

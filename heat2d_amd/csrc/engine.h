@@ -254,6 +254,7 @@ class Engine {
   };
   struct UnitLists {
     int H = 0;
+    int tag[4] = {0, 0, 0, 0};  // integrity tags of d_all, d_interior, d_boundary, d_bfirst
     Unit* d_all = nullptr;
     Unit* d_interior = nullptr;
     Unit* d_boundary = nullptr;
@@ -291,7 +292,6 @@ class Engine {
   void run_direct(RunStats& st, int64_t target);
   void run_signal(RunStats& st, int64_t target);
   void run_serial(RunStats& st, int64_t target);
-  CopyDesc* local_descs(int K, int& n, int64_t& maxe);
   void check_tile(int t) const;
   void trace_begin(const char* phase, hipStream_t s);
   void trace_end(const char* phase, hipStream_t s);
@@ -316,9 +316,25 @@ class Engine {
   hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_t0_ = nullptr, ev_t1_ = nullptr, ev_done_ = nullptr;
   void end_of_run_wait(RunStats& st, std::chrono::steady_clock::time_point w0);
   std::map<std::pair<int, int>, UnitLists> units_;
-  std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> local_descs_;  // (K, parity)
-  std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> pack_descs_;   // (K, parity) for rccl
-  std::map<std::pair<int, int>, std::tuple<CopyDesc*, int, int64_t>> unpack_descs_;
+  // an uploaded copy-descriptor list: n descriptors, the largest rectangle, its integrity tag
+  struct DescList {
+    CopyDesc* d = nullptr;
+    int n = 0;
+    int64_t maxe = 0;
+    int64_t tag = 0;
+  };
+  DescList upload_descs(std::vector<CopyDesc>& v);  // tags and uploads (GPU) or keeps (CPU) a list
+  const DescList& local_descs(int K);
+  void local_copy(const DescList& D, hipStream_t s);  // one local exchange (tagged, counted on compute_)
+  std::map<std::pair<int, int>, DescList> local_descs_;  // (K, parity)
+  std::map<std::pair<int, int>, DescList> pack_descs_;   // (K, parity) for rccl
+  std::map<std::pair<int, int>, DescList> unpack_descs_;
+  // ---- integrity checks (kInteg* bits of the device error word, named by poll_abort) ----
+  unsigned long long lid_ = 0;                  // streaming launches enqueued (launch ids)
+  unsigned long long* d_lid_seen_ = nullptr;    // highest launch id a launch has completed
+  unsigned long long* d_copies_done_ = nullptr;  // local exchange copy blocks completed (compute stream)
+  unsigned long long copies_need_ = 0;          // ... enqueued
+  static int next_tag();                        // process-wide plan tags (never 0)
   unsigned long long* d_wait_acc_ = nullptr;  // StreamArgs::wait_acc (3 words)
   unsigned long long* d_stamps_ = nullptr;    // StreamArgs::stamps ring (timeline diagnostics)
   static constexpr int kTimelineUnits = 8192; // units recorded per launch at most

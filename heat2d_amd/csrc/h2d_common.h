@@ -135,6 +135,7 @@ struct CopyDesc {
   int64_t dst_pitch;
   int64_t rows;
   int64_t cols;
+  int64_t tag = 0;  // integrity tag of the descriptor list (launch_copy_rects)
 };
 
 }  // namespace h2d

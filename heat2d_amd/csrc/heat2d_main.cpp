@@ -7,6 +7,7 @@
 // grad1612_cuda_heat.cu:6-13) with runtime flags; banners follow C-IO-4.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -325,8 +326,6 @@ int main(int argc, char** argv) {
   const std::string tsel = a.count("transport") ? a["transport"] : "auto";
   if (world > 1) {
     o.ranks = {env.rank};
-    // ranks sharing a GPU: no persistent launches (each needs every one of its waves resident)
-    if (world > std::max(1, ndev)) o.persistent = 0;
     if (dev != "gpu") o.transport = kTransportExternal;
     // direct IPC needs halo units of at least max(K, G) rows at both ends of every strip (and,
     // for 2-D blocks, tiles 4-column aligned: the engine refuses others and every rank falls
@@ -350,6 +349,16 @@ int main(int argc, char** argv) {
   try {
     Bootstrap boot(env.rank, world, env.addr, env.port);
     std::unique_ptr<ShmBarrier> shm = node_barrier(boot);
+    if (world > 1 && o.device >= 0) {
+      // ranks on one physical GPU (host + PCI bus id, whatever the visibility setup): no
+      // persistent launches on any rank (each needs every one of its waves resident)
+      char host[256] = {0}, bus[64] = {0};
+      gethostname(host, sizeof(host) - 1);
+      H2D_HIP_CHECK(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, o.device));
+      std::vector<std::string> ids = boot.allgather(std::string(host) + "|" + bus);
+      std::sort(ids.begin(), ids.end());
+      if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) o.persistent = 0;
+    }
     std::unique_ptr<Engine> ep;
     std::string why;
     try {

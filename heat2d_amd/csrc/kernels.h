@@ -43,6 +43,9 @@ struct Unit {
   int flags;
   int cb, olo, ohi;
   int links;
+  // integrity tag of the unit list this unit was uploaded in (StreamArgs::utag): a wave that
+  // reads a unit of another list (a stale upload, a reused allocation) reports it and stops
+  int tag = 0;
 };
 constexpr int kEdgeCols = 1, kEdgeRows = 2, kUnitReverse = 4, kUnitSigEnd = 8, kUnitNS = 16;
 // side links, indexed like Dir - 2 (kW .. kSE)
@@ -101,8 +104,21 @@ struct DecideArgs {
   unsigned long long seq = 0;
 };
 
+// Integrity bits of the engine's device error word (StreamArgs::timed_out, shared with the
+// bounded-wait timeouts 1/2/4/8): a launch that sees inconsistent inputs reports instead of
+// computing on them, and the host names the cause (Engine::poll_abort).
+constexpr unsigned kIntegArgs = 16u;     // kernel arguments torn: head and tail launch ids differ
+constexpr unsigned kIntegUnits = 32u;    // a unit's tag is not the tag of the list the launch names
+constexpr unsigned kIntegReplay = 64u;   // a launch ran with the arguments of an earlier launch
+constexpr unsigned kIntegDescs = 128u;   // a copy descriptor's tag is not the list's tag
+constexpr unsigned kIntegOrder = 256u;   // a stencil launch started before its exchange copy finished
+
 // Arguments of the temporally-blocked streaming stencil.
 struct StreamArgs {
+  // launch id (engine launches: > 0, increasing in stream order; 0: no integrity checks).  The
+  // same id is the struct's LAST member too, so the two ends of the kernel-argument block are
+  // compared by every wave.
+  unsigned long long lid = 0;
   const float* src;
   float* dst;
   const Unit* units;
@@ -176,6 +192,14 @@ struct StreamArgs {
   // end, hardware id (XCC_ID << 16 | HW_ID[15:0])}.
   unsigned long long* wait_acc = nullptr;
   unsigned long long* stamps = nullptr;
+  // integrity (lid > 0): the tag every unit of `units` carries; the engine's highest launch id
+  // seen (wave 0 raises it at its end — an old value >= lid is a replayed launch); serial
+  // pipeline: the exchange copy blocks completed so far must equal copies_need at wave 0's start
+  int utag = 0;
+  unsigned long long* lid_seen = nullptr;
+  const unsigned long long* copies_done = nullptr;
+  unsigned long long copies_need = 0;
+  unsigned long long lid_tail = 0;
 };
 
 // ---- persistent pipelined streaming stencil (pstream_kernel.hpp) ---------------------------
@@ -256,7 +280,14 @@ void launch_naive_step(const TileGeom& g, const float* src, float* dst, int prec
                        double cy, bool per_x, bool per_y, hipStream_t s);
 void launch_init(const TileGeom& g, float* base, int init, hipStream_t s);
 void launch_poison(const TileGeom& g, float* base, bool fixed, bool per_x, bool per_y, hipStream_t s);
-void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s);
+// tag != 0: every descriptor must carry it (else kIntegDescs is reported through integ /
+// integ_host and the block copies nothing); done != nullptr: each block adds 1 when its copies
+// are issued and drained (the serial pipeline's ordering check, StreamArgs::copies_done).
+void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s, int64_t tag = 0,
+                       unsigned long long* done = nullptr, unsigned int* integ = nullptr,
+                       unsigned int* integ_host = nullptr);
+// blocks launch_copy_rects uses for (ndesc, max_elems): what a `done` counter advances by
+int64_t copy_rects_blocks(int ndesc, int64_t max_elems);
 void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s);
 // One wave polls *counter (system-scope acquire loads, s_sleep between polls) until it reaches
 // `target`; after `max_polls` it gives up and sets *timed_out (the caller reports it).

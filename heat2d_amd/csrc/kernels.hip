@@ -48,12 +48,24 @@ __global__ void poison_kernel(TileGeom g, float* __restrict__ base, int fixed, i
   }
 }
 
-__global__ void copy_rects_kernel(const CopyDesc* __restrict__ descs) {
+__global__ void copy_rects_kernel(const CopyDesc* __restrict__ descs, int64_t tag, unsigned long long* done,
+                                  unsigned int* integ, unsigned int* integ_host) {
   const CopyDesc d = descs[blockIdx.y];
-  const int64_t total = d.rows * d.cols;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / d.cols, cc = e - r * d.cols;
-    d.dst[r * d.dst_pitch + cc] = d.src[r * d.src_pitch + cc];
+  if (tag != 0 && d.tag != tag) {
+    // a descriptor of another list (stale upload / reused allocation): copy nothing, report
+    if (threadIdx.x == 0) report_timeout(integ, integ_host, kIntegDescs);
+  } else {
+    const int64_t total = d.rows * d.cols;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t r = e / d.cols, cc = e - r * d.cols;
+      d.dst[r * d.dst_pitch + cc] = d.src[r * d.src_pitch + cc];
+    }
+  }
+  if (done != nullptr) {
+    // every thread's stores acknowledged, then one count for the block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -717,10 +729,17 @@ void launch_poison(const TileGeom& g, float* base, bool fixed, bool per_x, bool 
   H2D_HIP_CHECK(hipGetLastError());
 }
 
-void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s) {
+int64_t copy_rects_blocks(int ndesc, int64_t max_elems) {
+  if (ndesc <= 0 || max_elems <= 0) return 0;
+  return std::min<int64_t>((max_elems + 255) / 256, 1024) * (int64_t)ndesc;
+}
+
+void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s, int64_t tag,
+                       unsigned long long* done, unsigned int* integ, unsigned int* integ_host) {
   if (ndesc <= 0 || max_elems <= 0) return;
   const unsigned bx = (unsigned)std::min<int64_t>((max_elems + 255) / 256, 1024);
-  hipLaunchKernelGGL(copy_rects_kernel, dim3(bx, (unsigned)ndesc), dim3(256), 0, s, d_descs);
+  hipLaunchKernelGGL(copy_rects_kernel, dim3(bx, (unsigned)ndesc), dim3(256), 0, s, d_descs, tag, done, integ,
+                     integ_host);
   H2D_HIP_CHECK(hipGetLastError());
 }
 

@@ -472,6 +472,19 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   const bool stamping = a.stamps != nullptr;  // diagnostics: per-wave timeline
   const unsigned long long t_start = stamping ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const Unit u = a.units[w];
+  if (a.lid != 0ull) {
+    // integrity (wave-uniform, scalar): both ends of the argument block name this launch, the
+    // unit comes from the list the launch names, and (serial pipeline) the exchange copy in
+    // front of this launch has finished — else report and compute nothing
+    unsigned bad = a.lid_tail != a.lid ? kIntegArgs : u.tag != a.utag ? kIntegUnits : 0u;
+    if (bad == 0u && w == 0 && a.copies_done != nullptr &&
+        __hip_atomic_load(a.copies_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.copies_need)
+      bad = kIntegOrder;
+    if (bad != 0u) {
+      if (lane == 0) report_timeout(a.timed_out, a.timed_out_host, bad);
+      return;
+    }
+  }
   const bool halo_unit = w < a.nsignal;
   const bool ns_unit = halo_unit && (u.flags & kUnitNS) != 0;  // top / bottom halo unit of its strip
   const int dir = (u.flags & kUnitReverse) ? 1 : 0;  // 0: north halo (top unit), 1: south (bottom unit)
@@ -662,6 +675,12 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     int slot = w + a.prot;
     if (slot >= a.nunits) slot -= a.nunits;
     publish_partial(a.partials, slot, racc, a.nunits, a.dec, lane);
+  }
+  if (w == 0 && lane == 0 && a.lid_seen != nullptr) {
+    // replay check: launch ids rise in stream order, so an older or equal id seen already means
+    // this launch ran with the arguments of an earlier one
+    if (__hip_atomic_fetch_max(a.lid_seen, a.lid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.lid)
+      report_timeout(a.timed_out, a.timed_out_host, kIntegReplay);
   }
   if (stamping) {
     // the wave's stores have drained: its work is done, not just issued

@@ -145,6 +145,21 @@ class DistContext:
         dist.gather_object(obj, out, dst=dst)
         return out
 
+    def devices_shared(self, device: int, pci_id: str) -> bool:
+        """Collective: True if any two ranks run on the same physical GPU (same host and PCI bus
+        id).  Ordinals and visibility masks cannot tell: two ranks may name the same device
+        explicitly, or see one GPU each under different numbering.  Sets ``distinct_devices``."""
+        if not self.is_multi:
+            self.distinct_devices = device >= 0
+            return False
+        import socket
+
+        ident = f"{socket.gethostname()}|{pci_id}" if device >= 0 else f"cpu|{self.rank}"
+        ids = self.all_gather_bytes(ident.encode())
+        shared = device >= 0 and len(set(ids)) < len(ids)
+        self.distinct_devices = device >= 0 and not shared
+        return shared
+
     def get_nccl_group(self):
         """Lazily created RCCL-backed group for the torch p2p transport on GPUs."""
         if self.nccl_group is None:

@@ -127,6 +127,10 @@ class Solver:
             torch.cuda.set_device(self.device)
         else:
             self.device = -1
+        # ranks on one physical GPU (collective; any visibility setup): persistent launches off on
+        # every rank together unless forced, so all ranks' IPC handles carry the same plans
+        self.shared_gpu = (world > 1 and self.on_gpu and
+                           self.ctx.devices_shared(self.device, n.device_pci_id(self.device)))
         self.transport = transport
         self.tuned = None
         self.engine_kw = {}
@@ -203,9 +207,14 @@ class Solver:
         if cfg.pipeline not in PIPELINE_OPTIONS:
             raise ValueError(f"unknown pipeline {cfg.pipeline!r}")
         kw.update(PIPELINE_OPTIONS[cfg.pipeline])
-        if self.device >= 0 and self.ctx.world > max(1, n.device_count()):
+        if cfg.persistent not in ("auto", "on", "off"):
+            raise ValueError(f"unknown persistent mode {cfg.persistent!r}")
+        if cfg.persistent != "auto":
+            kw["persistent"] = 1 if cfg.persistent == "on" else 0
+        elif getattr(self, "shared_gpu", False):
             # ranks share a GPU: a persistent launch needs every one of its waves resident, which
             # another rank's persistent launch on the same GPU could prevent — launch per chunk
+            # (persistent="on" keeps it: a rehearsal whose ranks' plans fit the GPU together)
             kw["persistent"] = 0
         kw.update(getattr(self, "engine_kw", {}))
         return n.Engine(

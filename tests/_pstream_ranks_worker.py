@@ -17,6 +17,17 @@ rank = dist.get_rank()
 nx, ny, K, steps = 2 * 192 + 1, 2048, 8, 5 * 8 + 3
 e = n.Engine(nx, ny, gridx=2, gridy=1, tblock=K, device=0, ranks=[rank], transport=n.TRANSPORT_IPC,
              halo_timeout_s=10.0, persistent=1, pstream_cols=128)
+# Both ranks' persistent launches share the GPU and each needs all of its waves resident: run
+# only if the two plans fit on the device together, else report a skip.
+blocks = (len(e.pstream_units(K)) + 3) // 4
+allb = [None, None]
+dist.all_gather_object(allb, blocks)
+cap = n.device_props(0)["multiprocessor_count"] * n.pstream_blocks_per_cu(K, 0, 2)
+if sum(allb) > cap:
+    print(json.dumps({"rank": rank, "skip": f"plans need {sum(allb)} blocks, the GPU holds {cap}"}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.exit(0)
 hs = [None, None]
 dist.all_gather_object(hs, e.ipc_handle())
 e.ipc_open(hs)

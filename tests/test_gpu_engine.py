@@ -437,15 +437,7 @@ def _gather(eng, nx, ny):
 
 @pytest.mark.parametrize("gx,gy", [(1, 1), (2, 1), (1, 2)])
 @pytest.mark.parametrize("pipeline", [0, 3, 4, 5, 6])
-def test_fused_convergence_matches_oracle(native, gpu, gx, gy, pipeline, request):
-    if pipeline == 0 and gx * gy > 1:
-        # Known intermittent failure (round 3, docs/ARCHITECTURE.md "Known issues"): in the full GPU
-        # suite (~500 engines created earlier in the process) this local two-tile serial run has
-        # computed wrong tiles in about half of the suite runs, never when run alone or in the
-        # stress/bisect tools (tools/stress_flaky.py, tools/stress_seq.py, tools/bisect_conv.sh).
-        # The failure diagnostics below stay in place; not strict, so a pass is reported as XPASS.
-        request.applymarker(pytest.mark.xfail(reason="intermittent in long GPU test processes (local multi-tile "
-                                                     "serial pipeline); under investigation", strict=False))
+def test_fused_convergence_matches_oracle(native, gpu, gx, gy, pipeline):
     nx, ny = 257, 509
     ref = oracle(native, nx, ny, 3000, 1, **CONV)
     assert ref["converged"] and ref["steps_done"] == 98
