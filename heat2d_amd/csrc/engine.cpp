@@ -644,7 +644,8 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     if (residual && !recompute_rollback()) a.keep = tl.keep;
   }
   // integrity: launch id at both ends of the arguments, the list's tag, the device error word
-  a.lid = a.lid_tail = ++lid_;
+  a.lid = a.lid_tail = (opt_.debug_kernel & 2) ? 0ull : ++lid_;
+  a.dbg = opt_.debug_kernel;
   a.utag = L.tag[which];
   a.lid_seen = d_lid_seen_;
   a.timed_out = d_sig_timeout_;
@@ -1582,6 +1583,8 @@ void Engine::launch_pstream_chunks(int K, int J) {
   a.cx = opt_.cx;
   a.cy = opt_.cy;
   a.fixed = opt_.boundary == kFixed;
+  a.per_x = opt_.periodic_x;
+  a.per_y = opt_.periodic_y;
   a.dummy = d_dummy_;
   a.halo_polls = std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6));
   a.timed_out = d_sig_timeout_;
@@ -1862,6 +1865,20 @@ std::vector<float> Engine::download(int t) const {
   } else {
     for (int64_t i = 0; i < T.g.xcell; ++i)
       std::memcpy(&out[(size_t)(i * T.g.ycell)], T.buf[T.cur] + T.g.idx(i, 0), T.g.ycell * sizeof(float));
+  }
+  return out;
+}
+
+std::vector<float> Engine::storage(int t, int b) const {
+  check_tile(t);
+  if (b != 0 && b != 1) throw std::invalid_argument("storage: buffer 0 or 1");
+  const Tile& T = tiles_[t];
+  std::vector<float> out((size_t)T.g.elems());
+  if (on_gpu()) {
+    H2D_HIP_CHECK(hipStreamSynchronize(compute_));
+    H2D_HIP_CHECK(hipMemcpy(out.data(), T.buf[b], out.size() * sizeof(float), hipMemcpyDeviceToHost));
+  } else {
+    std::copy(T.buf[b], T.buf[b] + out.size(), out.begin());
   }
   return out;
 }

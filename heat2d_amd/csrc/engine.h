@@ -106,6 +106,8 @@ struct EngineOptions {
   // streaming launches of each run (0: off).  Read back with Engine::timeline().
   int timeline = 0;
   bool poison = false;        // debug canary: NaN in every cell no valid update may read
+  // diagnostics: 1 every streaming unit runs the halo-unit bodies; 2 no integrity checks (launch id 0)
+  int debug_kernel = 0;
   bool convergence = false;
   int64_t interval = 20;
   double sensitivity = 0.1;
@@ -213,6 +215,10 @@ class Engine {
   void set_steps_done(int64_t s) { steps_done_ = s; }
 
   std::vector<float> download(int t) const;  // owned block, row-major xcell×ycell
+  // diagnostics: the whole padded storage of buffer b (0/1) of tile t (srows × pitch), and which
+  // buffer is current
+  std::vector<float> storage(int t, int b) const;
+  int current_buffer(int t) const { return tiles_.at(t).cur; }
   void upload(int t, const float* owned);
   void synchronize() const;
 

@@ -196,6 +196,7 @@ struct StreamArgs {
   // seen (wave 0 raises it at its end — an old value >= lid is a replayed launch); serial
   // pipeline: the exchange copy blocks completed so far must equal copies_need at wave 0's start
   int utag = 0;
+  int dbg = 0;  // diagnostics (EngineOptions::debug_kernel): 1 every unit runs the halo bodies
   unsigned long long* lid_seen = nullptr;
   const unsigned long long* copies_done = nullptr;
   unsigned long long copies_need = 0;
@@ -232,6 +233,7 @@ struct PStreamArgs {
   int64_t gx0, gy0, NX, NY;
   double cx, cy;
   int fixed;
+  int per_x = 0, per_y = 0;
   float* dummy;
   // direct (IPC) halo units, per direction (0 north / top band, 1 south / bottom band, reverse)
   // and receive-buffer parity: chunk j reads parity (ipar0 + j) & 1 and pushes to the other

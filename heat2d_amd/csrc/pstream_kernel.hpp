@@ -110,7 +110,9 @@ __device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int la
   if (lane == 0) __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <int K, bool F32, int EDGE, bool FIXED, int CPL>
+// PUSH: a direct-pipeline halo unit (copies its first rows to the neighbour GPU each chunk); the
+// other units' steady loop carries no per-row push check.
+template <int K, bool F32, int EDGE, bool FIXED, int CPL, bool PUSH>
 __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w, int lane, PSlot& sl) {
   typedef typename LaneVec<CPL>::T V;
   // rows per steady iteration (8 for 2-column lanes was measured slower: 512x4096 K=8 2.21 vs
@@ -140,9 +142,12 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   LaneCtx c;
   c.gxb = a.gx0 + xin;
   c.dir = rev ? -1 : 1;
-  c.NX = a.NX;
+  c.rlo = a.per_x ? INT64_MIN : 0;
+  c.rhi = a.per_x ? (a.fixed ? INT64_MIN : INT64_MAX) : (a.fixed ? a.NX - 1 : a.NX);
   const int64_t gc = a.gy0 + cb;
-  auto colmask = [&](int64_t q) { return a.fixed ? (q == 0 || q == a.NY - 1) : (q < 0 || q >= a.NY); };
+  auto colmask = [&](int64_t q) {
+    return a.per_y ? false : a.fixed ? (q == 0 || q == a.NY - 1) : (q < 0 || q >= a.NY);
+  };
   c.m0 = colmask(gc + 0);
   c.m1 = colmask(gc + 1);
   c.m2 = CPL > 2 && colmask(gc + 2);
@@ -165,7 +170,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   c.xdir = rev ? -1 : 1;
   c.xlo = a.G;
   c.xhi = a.xcell - a.G;
-  const bool pushes = ns && a.push[dir][0] != nullptr;
+  const bool pushes = PUSH && ns && a.push[dir][0] != nullptr;
   c.prows = pushes ? a.sig_rows : 0;
   const int64_t in_base = (a.G + x0 - K) * a.pitch + a.PL + u.cb;  // lowest input row, lane 0
   const int64_t out_base = (a.G + x0) * a.pitch + a.PL + u.cb;     // lowest output row, lane 0
@@ -263,7 +268,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
 #pragma unroll
     for (int d = 0; d < RI; ++d) pf[d] = load_row_sc1<V>(rin, lvoff, soff(min(2 * K + d, n - 1)));
     __builtin_amdgcn_sched_barrier(0);
-    prologue<K, F32, EDGE, FIXED, false, true, false, 0>(S, pro, c, k, racc);
+    prologue<K, F32, EDGE, FIXED, false, true, false, PUSH, 0>(S, pro, c, k, racc);
     lap(4);
 
     int ir0 = 2 * K;
@@ -275,7 +280,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   {                                                                                   \
     const V nw = pf[D];                                                               \
     pf[D] = load_row_sc1<V>(rin, lvoff, soff(min(ir0 + (D) + RI, n - 1)));            \
-    process_row<K, F32, EDGE, FIXED, false, true, false, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
+    process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
     int it = 0;
     for (; ir0 + RI <= n; ir0 += RI) {
@@ -308,14 +313,14 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       }
     }
 #undef H2D_PSTEADY
-    if (ir0 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[0], ir0, c, k, racc);
-    if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
-    if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
+    if (ir0 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 0, K>(S, pf[0], ir0, c, k, racc);
+    if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
+    if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
     if constexpr (RI == 8) {
-      if (ir0 + 3 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 1, K>(S, pf[3], ir0 + 3, c, k, racc);
-      if (ir0 + 4 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[4], ir0 + 4, c, k, racc);
-      if (ir0 + 5 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 1, K>(S, pf[5], ir0 + 5, c, k, racc);
-      if (ir0 + 6 < n) process_row<K, F32, EDGE, FIXED, false, true, false, 0, K>(S, pf[6], ir0 + 6, c, k, racc);
+      if (ir0 + 3 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 1, K>(S, pf[3], ir0 + 3, c, k, racc);
+      if (ir0 + 4 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 0, K>(S, pf[4], ir0 + 4, c, k, racc);
+      if (ir0 + 5 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 1, K>(S, pf[5], ir0 + 5, c, k, racc);
+      if (ir0 + 6 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 0, K>(S, pf[6], ir0 + 6, c, k, racc);
     }
     if (have_poll) sl.known = max(sl.known, polled);
     // pushes not yet signalled at an iteration top: at the next chunk start (or launch end)
@@ -357,19 +362,27 @@ __global__ __launch_bounds__(256) void pstream_kernel(PStreamArgs a) {
   }
   sl.known = 0u;
   const bool fixed = a.fixed != 0;
+  if ((u.flags & kUnitNS) != 0 && a.push[(u.flags & kUnitReverse) ? 1 : 0][0] != nullptr) {
+    // direct-pipeline halo units: plain or fully masked bodies (masks are a no-op where the
+    // flags say no edge, periodic dimensions included)
+    if ((u.flags & 3) == 0) prun<K, F32, 0, false, CPL, true>(a, u, w, lane, sl);
+    else if (fixed) prun<K, F32, 3, true, CPL, true>(a, u, w, lane, sl);
+    else prun<K, F32, 3, false, CPL, true>(a, u, w, lane, sl);
+    return;
+  }
   switch (u.flags & 3) {
-    case 0: prun<K, F32, 0, false, CPL>(a, u, w, lane, sl); break;
+    case 0: prun<K, F32, 0, false, CPL, false>(a, u, w, lane, sl); break;
     case 1:
-      if (fixed) prun<K, F32, 1, true, CPL>(a, u, w, lane, sl);
-      else prun<K, F32, 1, false, CPL>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 1, true, CPL, false>(a, u, w, lane, sl);
+      else prun<K, F32, 1, false, CPL, false>(a, u, w, lane, sl);
       break;
     case 2:
-      if (fixed) prun<K, F32, 2, true, CPL>(a, u, w, lane, sl);
-      else prun<K, F32, 2, false, CPL>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 2, true, CPL, false>(a, u, w, lane, sl);
+      else prun<K, F32, 2, false, CPL, false>(a, u, w, lane, sl);
       break;
     default:
-      if (fixed) prun<K, F32, 3, true, CPL>(a, u, w, lane, sl);
-      else prun<K, F32, 3, false, CPL>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 3, true, CPL, false>(a, u, w, lane, sl);
+      else prun<K, F32, 3, false, CPL, false>(a, u, w, lane, sl);
       break;
   }
 }

@@ -130,7 +130,9 @@ __device__ __forceinline__ float2 row_update(const float2& P, const float2& C, c
 struct LaneCtx {
   int64_t gxb;     // global row of stream input index 0
   int64_t dir;     // +1: rows stream top-down, -1: bottom-up (kUnitReverse)
-  int64_t NX;
+  // global-edge rows: fixed -> rows rlo and rhi are held; ghost-zero -> rows < rlo or >= rhi are
+  // zero (a periodic dimension: bounds no row reaches, so the masked bodies are a safe superset)
+  int64_t rlo, rhi;
   bool m0, m1, m2, m3;  // per-column mask: fixed -> hold (global edge), ghost-zero -> zero (outside)
   float* sout;     // real output pointer (lanes in the output range), or a dummy slot
   int64_t spitch;  // row pitch of sout (0 for the dummy slot)
@@ -178,13 +180,37 @@ __device__ __forceinline__ void side_push(const float4& o, int64_t orow, const L
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Wide-store data hazard (gfx950, ROCm 7.2 hipcc).  A store of more than 64 bits reads its data
+// VGPRs after it issues, so a write of those VGPRs needs 2 wait states after the store.  hipcc
+// does not pad a 64-bit VALU write there (v_pk_add_f32, v_mov_b64, v_cvt_f64_f32, v_add_f64 right
+// after a buffer_store_dwordx4: tools/hazard_lint.py found 1 242 such pairs in the stencil
+// objects).  Under memory load the store then writes the new value for some lanes — measured:
+// element 1 of lanes 12-15 of every 16 in one row per unit (2-step 257x509 run), and the
+// intermittent wrong tiles of round 3 (the residual launches convert each stored row to fp64 in
+// place).  Every wide store is followed by `s_nop 1` that reads its data registers, so they stay
+// unchanged until two wait states after the store (the lint checks the built code objects).
+__device__ __forceinline__ void store_guard(const u32x4& d) { asm volatile("s_nop 1" ::"v"(d) : "memory"); }
+
+__device__ __forceinline__ u32x4 as_u32x4(const float4& o) {
+  return u32x4{__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(o.w)};
+}
+
+// Plain wide store of a lane's cells (16 B guarded; 8 B needs no guard).
+__device__ __forceinline__ void store_cells(float* p, const float4& o) {
+  const u32x4 d = as_u32x4(o);
+  *reinterpret_cast<u32x4*>(p) = d;
+  store_guard(d);
+}
+__device__ __forceinline__ void store_cells(float* p, const float2& o) { *reinterpret_cast<float2*>(p) = o; }
+
 // Store one lane's float4 of an output row write-through (buffer_store_dwordx4 ... sc1):
 // 16-B sc1 stores cost about a plain store, and leave no dirty line in the L2.  The resource is
 // loop-invariant (the unit's base); the row moves through the scalar offset.
 __device__ __forceinline__ void store_row_wt(float* base, unsigned voff, int soff, const float4& o) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-  const u32x4 d = {__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(o.w)};
+  const u32x4 d = as_u32x4(o);
   __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)voff, soff, 16 /* sc1 */);
+  store_guard(d);
 }
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -223,13 +249,13 @@ __device__ __forceinline__ float4 apply_edge(float4 o, const float4& C, int64_t 
   if constexpr ((EDGE & 2) != 0) {
     // per component: a select of a whole float4 aggregate is lowered through scratch memory
     if constexpr (FIXED) {
-      const bool r = gr == 0 || gr == c.NX - 1;
+      const bool r = gr == c.rlo || gr == c.rhi;
       o.x = r ? C.x : o.x;
       o.y = r ? C.y : o.y;
       o.z = r ? C.z : o.z;
       o.w = r ? C.w : o.w;
     } else {
-      const bool r = gr < 0 || gr >= c.NX;
+      const bool r = gr < c.rlo || gr >= c.rhi;
       o.x = r ? 0.0f : o.x;
       o.y = r ? 0.0f : o.y;
       o.z = r ? 0.0f : o.z;
@@ -252,11 +278,11 @@ __device__ __forceinline__ float2 apply_edge(float2 o, const float2& C, int64_t 
   }
   if constexpr ((EDGE & 2) != 0) {
     if constexpr (FIXED) {
-      const bool r = gr == 0 || gr == c.NX - 1;
+      const bool r = gr == c.rlo || gr == c.rhi;
       o.x = r ? C.x : o.x;
       o.y = r ? C.y : o.y;
     } else {
-      const bool r = gr < 0 || gr >= c.NX;
+      const bool r = gr < c.rlo || gr >= c.rhi;
       o.x = r ? 0.0f : o.x;
       o.y = r ? 0.0f : o.y;
     }
@@ -268,8 +294,10 @@ __device__ __forceinline__ float2 apply_edge(float2 o, const float2& C, int64_t 
 // Slot parity P = ir & 1: S[l][P] holds level-l row (ir-l-2), S[l][1-P] holds row (ir-l-1).
 // Level t computes row (ir - t) of level t.  Level K writes output row ir - 2K (unit-relative).
 // V: the lane's cells of a row (float4: 256-column strips; float2: 128-column strips, no
-// residual / side pushes).
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int P, int TMAX, class V>
+// residual / side pushes).  PUSH: the unit may copy output rows into a neighbour's receive buffer
+// (halo units only: the check is a branch per row, which would split the straight-line steady
+// loop of every other unit into per-row blocks the scheduler cannot overlap).
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, bool PUSH, int P, int TMAX, class V>
 __device__ __forceinline__ void process_row(V (&S)[K][2], V cur, int ir, const LaneCtx& c, const Coef& k,
                                             double& racc) {
 #pragma unroll
@@ -286,11 +314,12 @@ __device__ __forceinline__ void process_row(V (&S)[K][2], V cur, int ir, const L
     if (t == K) {
       const int64_t orow = ir - 2 * K;
       if constexpr (WT) store_row_wt(c.obase, c.voff, c.obo + (int)orow * c.obs, o);
-      else *reinterpret_cast<V*>(c.sout + orow * c.spitch) = o;
-      if (orow < c.prows) *reinterpret_cast<V*>(c.pout + orow * c.ppitch) = o;  // uniform branch
+      else store_cells(c.sout + orow * c.spitch, o);
+      if constexpr (PUSH)
+        if (orow < c.prows) store_cells(c.pout + orow * c.ppitch, o);  // uniform branch
       if constexpr (SIDE) side_push(o, orow, c);
       if constexpr (RESID) {
-        *reinterpret_cast<float4*>(c.kout + orow * c.kpitch) = mid;
+        store_cells(c.kout + orow * c.kpitch, mid);
         racc += c.st0 ? sq_diff(o.x, mid.x) : 0.0;
         racc += c.st1 ? sq_diff(o.y, mid.y) : 0.0;
         racc += c.st2 ? sq_diff(o.z, mid.z) : 0.0;
@@ -302,12 +331,12 @@ __device__ __forceinline__ void process_row(V (&S)[K][2], V cur, int ir, const L
 }
 
 // Prologue row IR (compile-time): levels t <= IR/2 are primed, from rows already in registers.
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int IR, class V>
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, bool PUSH, int IR, class V>
 __device__ __forceinline__ void prologue(V (&S)[K][2], const V (&pro)[2 * K], const LaneCtx& c, const Coef& k,
                                          double& racc) {
   if constexpr (IR < 2 * K) {
-    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR & 1, IR / 2>(S, pro[IR], IR, c, k, racc);
-    prologue<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR + 1>(S, pro, c, k, racc);
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, PUSH, IR & 1, IR / 2>(S, pro[IR], IR, c, k, racc);
+    prologue<K, F32, EDGE, FIXED, RESID, WT, SIDE, PUSH, IR + 1>(S, pro, c, k, racc);
   }
 }
 
@@ -315,14 +344,14 @@ __device__ __forceinline__ void prologue(V (&S)[K][2], const V (&pro)[2 * K], co
 // (=1).  A/B at 4096^2, depth 7, alternating processes (tools/ab_so.py, profiles/ab_prologue_r3.txt):
 // us/step 1000 steps 7.67/7.84/7.79 inline vs 7.79/7.78/7.94 up front; 20 steps 8.36/8.44/8.52 vs
 // 8.41/8.53/8.64.
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, int IR>
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, bool PUSH, int IR>
 __device__ __forceinline__ void prologue_inline(float4 (&S)[K][2], const float4* __restrict__ rowp,
                                                 const float4* __restrict__ hrowp, int64_t pitch4, const LaneCtx& c,
                                                 const Coef& k, double& racc) {
   if constexpr (IR < 2 * K) {
     const float4 v = (IR < K ? hrowp : rowp)[(int64_t)IR * pitch4];
-    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR & 1, IR / 2>(S, v, IR, c, k, racc);
-    prologue_inline<K, F32, EDGE, FIXED, RESID, WT, SIDE, IR + 1>(S, rowp, hrowp, pitch4, c, k, racc);
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, PUSH, IR & 1, IR / 2>(S, v, IR, c, k, racc);
+    prologue_inline<K, F32, EDGE, FIXED, RESID, WT, SIDE, PUSH, IR + 1>(S, rowp, hrowp, pitch4, c, k, racc);
   }
 }
 
@@ -347,8 +376,9 @@ __device__ __forceinline__ void unit_signal(unsigned long long* sig, int lane, i
 }
 
 // sig_at > 0: signal (once) before processing stream row sig_at (a multiple of 4 past 2K),
-// i.e. once every output row < sig_at - 2K is stored.
-template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE>
+// i.e. once every output row < sig_at - 2K is stored.  HALO: the unit pushes rows or signals
+// (the halo units of the signalled / direct pipelines); other units' bodies have neither check.
+template <int K, bool F32, int EDGE, bool FIXED, bool RESID, bool WT, bool SIDE, bool HALO>
 __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const float4* __restrict__ hrowp,
                                          int64_t pitch4, int n, const LaneCtx& c, const Coef& k, double& racc,
                                          int sig_at, unsigned long long* sig, int lane) {
@@ -372,12 +402,12 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
 #pragma unroll
   for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(2 * K + d, n - 1) * pitch4];
   __builtin_amdgcn_sched_barrier(0);  // keep the loads above: each use waits only for its own row
-  prologue<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0>(S, pro, c, k, racc);
+  prologue<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 0>(S, pro, c, k, racc);
 #else
   float4 pf[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) pf[d] = rowp[(int64_t)min(2 * K + d, n - 1) * pitch4];
-  prologue_inline<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0>(S, rowp, hrowp, pitch4, c, k, racc);
+  prologue_inline<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 0>(S, rowp, hrowp, pitch4, c, k, racc);
 #endif
 
   int ir0 = 2 * K;  // even: slot parity of sub-step d is d & 1
@@ -385,10 +415,11 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
   {                                                                          \
     const float4 nw = pf[D];                                                 \
     pf[D] = rowp[(int64_t)min(ir0 + (D) + 4, n - 1) * pitch4];               \
-    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
   for (; ir0 + 4 <= n; ir0 += 4) {
-    if (ir0 == sig_at) unit_signal(sig, lane, c.rel);
+    if constexpr (HALO)
+      if (ir0 == sig_at) unit_signal(sig, lane, c.rel);
     H2D_STEADY(0)
     H2D_STEADY(1)
     H2D_STEADY(2)
@@ -396,12 +427,13 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
   }
 #undef H2D_STEADY
   // tail: at most 3 rows
-  if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0, K>(S, pf[0], ir0, c, k, racc);
-  if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
-  if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
+  if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 0, K>(S, pf[0], ir0, c, k, racc);
+  if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
+  if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
   // the loop visits every sig_at candidate below its exit value: a signal point at or past the
   // exit has not fired yet (unit shorter than its signal rows, or kUnitSigEnd)
-  if (sig_at >= ir0) unit_signal(sig, lane, c.rel);
+  if constexpr (HALO)
+    if (sig_at >= ir0) unit_signal(sig, lane, c.rel);
 }
 
 // A bounded wait gave up: set `bit` in the device word (fail-fast for later waits) and in its
@@ -418,12 +450,26 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-template <int K, bool F32, bool RESID, bool WT, int EDGE, bool SIDE = false>
+template <int K, bool F32, bool RESID, bool WT, int EDGE, bool SIDE, bool HALO>
 __device__ __forceinline__ void run_edge(const float4* rowp, const float4* hrowp, int64_t pitch4, int n,
                                          const LaneCtx& c, const Coef& k, double& racc, bool fixed, int sig_at,
                                          unsigned long long* sig, int lane) {
-  if (fixed) run_unit<K, F32, EDGE, true, RESID, WT, SIDE>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
-  else run_unit<K, F32, EDGE, false, RESID, WT, SIDE>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+  if (fixed) run_unit<K, F32, EDGE, true, RESID, WT, SIDE, HALO>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+  else run_unit<K, F32, EDGE, false, RESID, WT, SIDE, HALO>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+}
+
+// The bodies of the units that neither push nor signal (all but a few per launch): no per-row
+// check, so the steady loop is straight-line code.
+template <int K, bool F32, bool RESID, bool WT>
+__device__ __forceinline__ void run_plain(const Unit& u, const float4* rowp, const float4* hrowp, int64_t pitch4,
+                                          int n, const LaneCtx& c, const Coef& k, double& racc, bool fixed,
+                                          int sig_at, unsigned long long* sig, int lane) {
+  switch (u.flags & 3) {
+    case 0: run_unit<K, F32, 0, false, RESID, WT, false, false>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane); break;
+    case 1: run_edge<K, F32, RESID, WT, 1, false, false>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+    case 2: run_edge<K, F32, RESID, WT, 2, false, false>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+    default: run_edge<K, F32, RESID, WT, 3, false, false>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
+  }
 }
 
 // The decision of a convergence check, by the one lane that holds the total.
@@ -556,11 +602,12 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   LaneCtx c;
   c.gxb = a.gx0 + xin;
   c.dir = rev ? -1 : 1;
-  c.NX = a.NX;
   const int64_t gc = a.gy0 + cb;
   const bool fixed = a.fixed != 0;
+  c.rlo = a.per_x ? INT64_MIN : 0;
+  c.rhi = a.per_x ? (fixed ? INT64_MIN : INT64_MAX) : (fixed ? a.NX - 1 : a.NX);
   auto colmask = [&](int64_t q) {
-    return fixed ? (q == 0 || q == a.NY - 1) : (q < 0 || q >= a.NY);
+    return a.per_y ? false : fixed ? (q == 0 || q == a.NY - 1) : (q < 0 || q >= a.NY);
   };
   c.m0 = colmask(gc + 0);
   c.m1 = colmask(gc + 1);
@@ -649,15 +696,15 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   if (c.spu) {
     // side-pushing units of the 2-D direct pipeline: their own bodies, so the push code costs the
     // common bodies no registers (the host never gives such a unit a column-edge window)
-    if ((u.flags & 3) == 0) run_unit<K, F32, 0, false, RESID, WT, true>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
-    else run_edge<K, F32, RESID, WT, 2, true>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane);
+    if ((u.flags & 3) == 0) run_unit<K, F32, 0, false, RESID, WT, true, true>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+    else run_edge<K, F32, RESID, WT, 2, true, true>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane);
+  } else if (sig != nullptr || c.prows > 0 || (a.dbg & 1) != 0) {
+    // halo units (a few per launch): plain or fully masked bodies (the masks are a no-op wherever
+    // the unit's flags say no edge, periodic dimensions included)
+    if ((u.flags & 3) == 0) run_unit<K, F32, 0, false, RESID, WT, false, true>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane);
+    else run_edge<K, F32, RESID, WT, 3, false, true>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane);
   } else {
-    switch (u.flags & 3) {
-      case 0: run_unit<K, F32, 0, false, RESID, WT, false>(rowp, hrowp, pitch4, n, c, k, racc, sig_at, sig, lane); break;
-      case 1: run_edge<K, F32, RESID, WT, 1>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
-      case 2: run_edge<K, F32, RESID, WT, 2>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
-      default: run_edge<K, F32, RESID, WT, 3>(rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane); break;
-    }
+    run_plain<K, F32, RESID, WT>(u, rowp, hrowp, pitch4, n, c, k, racc, fixed, sig_at, sig, lane);
   }
   if (xpushes != 0) {
     // side and corner pushes are complete: drain, release as the N/S signal does, then one
@@ -676,7 +723,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     if (slot >= a.nunits) slot -= a.nunits;
     publish_partial(a.partials, slot, racc, a.nunits, a.dec, lane);
   }
-  if (w == 0 && lane == 0 && a.lid_seen != nullptr) {
+  if (w == 0 && lane == 0 && a.lid != 0ull && a.lid_seen != nullptr) {
     // replay check: launch ids rise in stream order, so an older or equal id seen already means
     // this launch ran with the arguments of an earlier one
     if (__hip_atomic_fetch_max(a.lid_seen, a.lid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.lid)

@@ -435,76 +435,100 @@ def _gather(eng, nx, ny):
     return out
 
 
+def _ranges(v):
+    v = sorted(set(int(x) for x in v))
+    out, a = [], None
+    for i, x in enumerate(v):
+        if a is None:
+            a = x
+        if i + 1 == len(v) or v[i + 1] != x + 1:
+            out.append(f"{a}-{x}" if a != x else f"{a}")
+            a = None
+    return ",".join(out[:12]) + ("..." if len(out) > 12 else "")
+
+
 @pytest.mark.parametrize("gx,gy", [(1, 1), (2, 1), (1, 2)])
 @pytest.mark.parametrize("pipeline", [0, 3, 4, 5, 6])
 def test_fused_convergence_matches_oracle(native, gpu, gx, gy, pipeline):
+    """Convergence (check every 9 steps) on every pipeline, fused (device-side) and host-synchronised
+    checks: the converged step, residual and grid of the oracle.  The run advances in 9-step pieces
+    (one check each, the same chunks as one long run) in lockstep with the CPU engine of the same
+    decomposition, so a divergence is caught at the piece where it happens."""
     nx, ny = 257, 509
     ref = oracle(native, nx, ny, 3000, 1, **CONV)
     assert ref["converged"] and ref["steps_done"] == 98
     for fused in (-1, 0):
         eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
                             small_grid_lds=False, tiled=0, **PIPELINES[pipeline], **CONV)
-        st = eng.run(3000)
-        if not (st["converged"] and st["steps_done"] == ref["steps_done"]):
-            # diagnose: is the grid wrong, or only the residual?
-            plain = oracle(native, nx, ny, int(st["steps_done"]), 1)["grid"]
-            got = _gather(eng, nx, ny)
-            bad = got != plain
-            r, c = np.nonzero(bad)
-            # a fresh engine of the same configuration, 9 steps at a time: where does it first go wrong?
-            e2 = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
-                               small_grid_lds=False, tiled=0, **PIPELINES[pipeline],
-                               **{**CONV, "sensitivity": 0.0})
-            first = None
-            for i in range(1, 40):
-                e2.run(1)
-                g2 = _gather(e2, nx, ny)
-                o2 = oracle(native, nx, ny, i, 1)["grid"]
-                b2 = g2 != o2
-                if b2.any():
-                    r2, c2 = np.nonzero(b2)
-                    first = (i, int(b2.sum()), int(r2.min()), int(r2.max()), int(c2.min()), int(c2.max()),
-                             float(np.abs(g2 - o2).max()))
-                    rows = sorted(set(r2.tolist()))
-                    print(f"rerun: wrong rows at step {i}: {rows[:40]}", flush=True)
-                    print(f"rerun: tile geoms {[e2.geom(t) for t in range(e2.num_tiles())]}", flush=True)
-                    break
-            print(f"rerun: first wrong (steps, cells, rows, cols, max|d|) {first}", flush=True)
-
-            def ranges(v):
-                v = sorted(set(int(x) for x in v))
-                out, a = [], None
-                for i, x in enumerate(v):
-                    if a is None:
-                        a = x
-                    if i + 1 == len(v) or v[i + 1] != x + 1:
-                        out.append(f"{a}-{x}" if a != x else f"{a}")
-                        a = None
-                return ",".join(out[:12]) + ("..." if len(out) > 12 else "")
-
-            for conv_on in (True, False):
-                for nsteps in (1, 2, 8, 9):
-                    kw3 = {**CONV, "sensitivity": 0.0} if conv_on else {}
-                    e3 = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
-                                       small_grid_lds=False, tiled=0, **PIPELINES[pipeline], **kw3)
-                    e3.run(nsteps)
-                    g3 = _gather(e3, nx, ny)
-                    o3 = oracle(native, nx, ny, nsteps, 1)["grid"]
-                    b3 = g3 != o3
-                    r3, c3 = np.nonzero(b3)
-                    print(f"diag conv={conv_on} steps={nsteps}: wrong {int(b3.sum())} rows {ranges(r3)} cols {ranges(c3)}"
-                          + (f" max|d| {np.abs(g3 - o3).max():.4g}" if b3.any() else ""), flush=True)
-                    del e3
-            pytest.fail(f"fused={fused}: converged {st['converged']} steps {st['steps_done']} residual "
-                        f"{st['residual']!r} (oracle {ref['residual']!r}); grid cells != oracle: {int(bad.sum())}"
-                        + (f" rows {r.min()}-{r.max()} cols {c.min()}-{c.max()} nan {int(np.isnan(got).sum())}"
-                           if bad.any() else "") + f"; path {st['path']} chunks {st['chunks']}")
+        cpu = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=-1, **CONV)
+        for piece in range(1, 40):
+            st, sc = eng.run(9), cpu.run(9)
+            got, want = _gather(eng, nx, ny), _gather(cpu, nx, ny)
+            if not np.array_equal(got, want) or st["converged"] != sc["converged"]:
+                bad = got != want
+                r, c = np.nonzero(bad)
+                per_tile = []
+                for t in range(eng.num_tiles()):
+                    g = eng.geom(t)
+                    bt = bad[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]]
+                    per_tile.append(int(bt.sum()))
+                pytest.fail(f"fused={fused}: piece {piece} (steps {9 * (piece - 1)}-{9 * piece}): wrong cells "
+                            f"{int(bad.sum())} per tile {per_tile} rows {_ranges(r)} cols {_ranges(c)}"
+                            + (f" max|d| {float(np.abs(got - want)[bad].max()):.4g}" if bad.any() else "")
+                            + f"; converged {st['converged']} vs {sc['converged']}, residual {st['residual']!r} "
+                              f"vs {sc['residual']!r}; path {st['path']} chunks {st['chunks']}")
+            if st["converged"]:
+                break
+        assert st["converged"] and st["steps_done"] == ref["steps_done"]
         assert abs(st["residual"] - ref["residual"]) <= 1e-9 * ref["residual"]
         assert np.array_equal(_gather(eng, nx, ny), ref["grid"]), (gx, gy, pipeline, fused)
         # continuing re-checks at step 99 against the converged state: converged again, same state
         st2 = eng.run(5)
         assert st2["converged"] and st2["steps_done"] == ref["steps_done"]
         assert np.array_equal(_gather(eng, nx, ny), ref["grid"])
+        del eng, cpu
+
+
+def _outside_nonzero(eng, t, b):
+    """Cells of buffer b of tile t that lie outside the global grid (ghost-zero: must stay 0)."""
+    g = eng.geom(t)
+    st = eng.storage(t, b)
+    G, PL = g["G"], g["PL"]
+    rows = np.arange(st.shape[0])[:, None] - G + g["gx0"]
+    cols = np.arange(st.shape[1])[None, :] - PL + g["gy0"]
+    out = (rows < 0) | (rows >= g["NX"]) | (cols < 0) | (cols >= g["NY"])
+    # only the ghost ring the stencil can read (G rows / PL columns around the owned block)
+    ring = (np.arange(st.shape[1])[None, :] < PL + g["ycell"] + G) & (np.arange(st.shape[1])[None, :] >= PL - G)
+    r, c = np.nonzero(out & ring & (st != 0))
+    return len(r), (_ranges(r - G), _ranges(c - PL)) if len(r) else None
+
+
+@pytest.mark.parametrize("gx,gy", [(2, 1), (1, 2)])
+def test_serial_tiles_long_convergence_run(native, gpu, gx, gy):
+    """The local two-tile serial pipeline with checks every 9 steps, as ONE run of up to 3000 steps
+    (fused and host-synchronised checks): converges at the oracle's step with its grid.  On a
+    mismatch it reports the wrong owned cells per tile and any non-zero cell of the zero ghost
+    ring in either buffer (a stray writer)."""
+    nx, ny = 257, 509
+    ref = oracle(native, nx, ny, 3000, 1, **CONV)
+    for fused in (-1, 0):
+        eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
+                            small_grid_lds=False, tiled=0, overlap=False, **CONV)
+        st = eng.run(3000)
+        got = _gather(eng, nx, ny)
+        if not (st["converged"] and st["steps_done"] == ref["steps_done"] and np.array_equal(got, ref["grid"])):
+            want = oracle(native, nx, ny, int(st["steps_done"]), 1)["grid"]
+            bad = got != want
+            lines = [f"fused={fused}: converged {st['converged']} steps {st['steps_done']} residual {st['residual']!r}"]
+            for t in range(eng.num_tiles()):
+                g = eng.geom(t)
+                bt = bad[g["gx0"]:g["gx0"] + g["xcell"], g["gy0"]:g["gy0"] + g["ycell"]]
+                r, c = np.nonzero(bt)
+                lines.append(f"tile {t} (cur {eng.current_buffer(t)}): wrong {int(bt.sum())} rows {_ranges(r)} cols "
+                             f"{_ranges(c)}; ring non-zero buf0 {_outside_nonzero(eng, t, 0)} buf1 "
+                             f"{_outside_nonzero(eng, t, 1)}")
+            pytest.fail("\n".join(lines))
+        del eng
 
 
 @pytest.mark.parametrize("interval", [1, 4, 8, 9, 20])

@@ -175,3 +175,16 @@ def test_bench_gate_all_candidates_fail_cpu(tmp_path):
     assert rec["error"] == "no transport passed the correctness gate"
     assert rec["gate"][0]["transport"] == "torch" and not rec["gate"][0]["ok"]
     assert "HEAT2D_GATE_FAIL" in rec["gate"][0]["detail"]
+
+
+@pytest.mark.parametrize("config,label", [("4096-strong", "rows8"), ("16384x8blocks", "blocks2x4")])
+def test_bench_eight_ranks_cpu_rehearsal(tmp_path, config, label):
+    """The driver's N=8 SCALE run, rehearsed on the host: 8 ranks under torch.distributed.run
+    (gloo), the BASELINE headline (4096^2 as 1-D row strips) and config 4 (2x4 blocks) at a small
+    side — one JSON line, the gate passed, every rank's tile == the single-rank grid."""
+    d = _bench(8, ["--gpus", "8", "--steps", "4", "--warmup", "1", "--side", "64", "--config", config,
+                   "--device", "cpu"], tmp_path)
+    assert d["n_gpus"] == 8 and d["steps"] == 4 and d["scaling"] == "strong"
+    assert d["config"]["parallelism"] == label and d["config"]["grid"] == [64, 64]
+    assert d["verified"] is True and d["gate"][0]["ok"]
+    assert abs(d["efficiency"] - d["speedup"] / 8) < 1e-12

@@ -24,6 +24,7 @@ step() {  # step NAME SECONDS CMD...: run, log, stop the script on failure
 for s in "$@"; do
   case "$s" in
     tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    tests-nox2) step tests-nox2 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
     tests-nox) step tests-nox 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
     engine-file) step engine-file 600 python -u -m pytest tests/test_gpu_engine.py -q --timeout 300 --timeout-method thread -rf ;;
     tests-k) step tests-k 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf -k "$TESTK" ;;
