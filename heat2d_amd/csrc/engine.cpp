@@ -1585,6 +1585,7 @@ void Engine::launch_pstream_chunks(int K, int J) {
   a.fixed = opt_.boundary == kFixed;
   a.per_x = opt_.periodic_x;
   a.per_y = opt_.periodic_y;
+  a.dbg = opt_.debug_kernel;
   a.dummy = d_dummy_;
   a.halo_polls = std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6));
   a.timed_out = d_sig_timeout_;

@@ -234,6 +234,7 @@ struct PStreamArgs {
   double cx, cy;
   int fixed;
   int per_x = 0, per_y = 0;
+  int dbg = 0;  // diagnostics (EngineOptions::debug_kernel): 1 every unit runs the halo-unit bodies
   float* dummy;
   // direct (IPC) halo units, per direction (0 north / top band, 1 south / bottom band, reverse)
   // and receive-buffer parity: chunk j reads parity (ipar0 + j) & 1 and pushes to the other

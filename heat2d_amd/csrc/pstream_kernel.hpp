@@ -75,8 +75,16 @@ __device__ __forceinline__ unsigned pneed(const PSlot& d, int A, int B, unsigned
   return cprev * (unsigned)d.hv + (unsigned)(d.qa + d.qs * r + 1);
 }
 
+// Progress words are accessed through global (address space 1) pointers: global_load / global_store
+// complete in issue order with the buffer loads and stores of the rows, so the counted
+// `s_waitcnt vmcnt(N)` of the publishing top stays valid, and hipcc waits for a poll's value with
+// a counted vmcnt instead of the vmcnt(0) + lgkmcnt(0) a flat (generic) access forces — a drain of
+// every outstanding row store at every iteration top (MI355X guide: flat_* return out of order).
+typedef __attribute__((address_space(1))) unsigned gu32;
+
 __device__ __forceinline__ unsigned ppoll(const PSlot& d, const unsigned* prog) {
-  return d.nb >= 0 ? __hip_atomic_load(prog + 32 * d.nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xffffffffu;
+  return d.nb >= 0 ? __hip_atomic_load((const gu32*)(prog + 32 * d.nb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0xffffffffu;
 }
 
 // Wait until every neighbour has published what rows [A, B) need (bounded).  false: gave up.
@@ -99,14 +107,17 @@ __device__ __forceinline__ bool pensure(PSlot& d, int A, int B, unsigned cprev, 
 }
 
 __device__ __forceinline__ void ppublish(unsigned* p, unsigned v, int lane) {
-  if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The direct pipeline's flag signal of a halo unit (its pushed rows' stores have completed).
+// The direct pipeline's flag signal of a halo unit.  The pushes are flat stores (the peer's
+// IPC-mapped buffer), which complete out of order with the counted vmcnt of the publishing top:
+// drain them (vmcnt and lgkmcnt) before the flag, whatever the release flavour.
 __device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int lane) {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   else if (rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  if (rel != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (rel != 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -170,7 +181,18 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   c.xdir = rev ? -1 : 1;
   c.xlo = a.G;
   c.xhi = a.xcell - a.G;
-  const bool pushes = PUSH && ns && a.push[dir][0] != nullptr;
+  // direction-resolved halo pointers: selects, not runtime-indexed kernel-argument arrays (a
+  // runtime index into the argument block made hipcc copy the whole block to scratch and reload
+  // fields from it at every iteration top)
+  const unsigned long long* const waitd = rev ? a.wait[1] : a.wait[0];
+  const unsigned long long need0 = rev ? a.need0[1] : a.need0[0];
+  const unsigned long long needinc = rev ? a.need_inc[1] : a.need_inc[0];
+  const float* const hsrc0 = rev ? a.hsrc[1][0] : a.hsrc[0][0];
+  const float* const hsrc1 = rev ? a.hsrc[1][1] : a.hsrc[0][1];
+  float* const push0 = rev ? a.push[1][0] : a.push[0][0];
+  float* const push1 = rev ? a.push[1][1] : a.push[0][1];
+  unsigned long long* const sigd = rev ? a.sig[1] : a.sig[0];
+  const bool pushes = PUSH && ns && push0 != nullptr;
   c.prows = pushes ? a.sig_rows : 0;
   const int64_t in_base = (a.G + x0 - K) * a.pitch + a.PL + u.cb;  // lowest input row, lane 0
   const int64_t out_base = (a.G + x0) * a.pitch + a.PL + u.cb;     // lowest output row, lane 0
@@ -202,18 +224,18 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   for (int j = 0; j < a.nchunks; ++j) {
     const unsigned cidx = a.cbase + (unsigned)j;
     const int par = (a.cur0 + j) & 1;
-    const float* src = a.buf[par];
-    float* dst = a.buf[par ^ 1];
+    const float* src = par ? a.buf[1] : a.buf[0];
+    float* dst = par ? a.buf[0] : a.buf[1];
     const int ipar = (a.ipar0 + j) & 1;
     if (j > 0) {
       // chunk start: my previous chunk's stores complete (the poll's wait drains them), publish
       // them, then the rows the up-front batch loads must be published by the neighbours
       lap(5);
       const unsigned pv = ppoll(sl, a.prog);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       ppublish(myprog, cidx * (unsigned)h, lane);
       if (sig_pending) {
-        psignal(a.sig[dir], a.rel, lane);
+        psignal(sigd, a.rel, lane);
         sig_pending = false;
       }
       sl.known = max(sl.known, pv);
@@ -222,13 +244,13 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       lap(2);
     }
     const V* hrowp = nullptr;
-    if (ns && a.wait[dir] != nullptr) {
+    if (ns && waitd != nullptr) {
       // the neighbour GPU's pushes of its chunk j-1 (this chunk's ghost rows)
       if (lane == 0 && !dead && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
-        const unsigned long long need = a.need0[dir] + (unsigned long long)j * a.need_inc[dir];
+        const unsigned long long need = need0 + (unsigned long long)j * needinc;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         long long i = 0;
-        while (__hip_atomic_load(a.wait[dir], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
+        while (__hip_atomic_load(waitd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
           if (++i > a.halo_polls) {
             report_timeout(a.timed_out, a.timed_out_host, 2u);
             break;
@@ -245,11 +267,11 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       if (a.acq == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       else if (a.acq == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      hrowp = reinterpret_cast<const V*>(a.hsrc[dir][ipar] + lane_in);
+      hrowp = reinterpret_cast<const V*>((ipar ? hsrc1 : hsrc0) + lane_in);
       lap(3);
     }
     c.obase = dst + out_base;
-    c.pout = (pushes && in_out) ? a.push[dir][ipar ^ 1] + xout * a.pitch + a.PL + cb : a.dummy + CPL * lane;
+    c.pout = (pushes && in_out) ? (ipar ? push0 : push1) + xout * a.pitch + a.PL + cb : a.dummy + CPL * lane;
     c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
     const __amdgpu_buffer_rsrc_t rin =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src) + in_base, (short)0, n * pb, 0x00020000);
@@ -291,7 +313,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);
         if (pushes && !signalled && issued_prev >= a.sig_rows) {  // the pushed rows have completed
-          psignal(a.sig[dir], a.rel, lane);
+          psignal(sigd, a.rel, lane);
           signalled = true;
         }
         if (have_poll) sl.known = max(sl.known, polled);
@@ -327,9 +349,9 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
     if (pushes && !signalled) sig_pending = true;
   }
   lap(5);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   ppublish(myprog, (a.cbase + (unsigned)a.nchunks) * (unsigned)h, lane);
-  if (sig_pending) psignal(a.sig[dir], a.rel, lane);
+  if (sig_pending) psignal(sigd, a.rel, lane);
   lap(1);
 #ifdef H2D_PSTREAM_PHASES
   if (tm && lane == 0) {
@@ -362,7 +384,8 @@ __global__ __launch_bounds__(256) void pstream_kernel(PStreamArgs a) {
   }
   sl.known = 0u;
   const bool fixed = a.fixed != 0;
-  if ((u.flags & kUnitNS) != 0 && a.push[(u.flags & kUnitReverse) ? 1 : 0][0] != nullptr) {
+  const bool halo = (u.flags & kUnitNS) != 0 && ((u.flags & kUnitReverse) ? a.push[1][0] : a.push[0][0]) != nullptr;
+  if (halo || (a.dbg & 1) != 0) {
     // direct-pipeline halo units: plain or fully masked bodies (masks are a no-op where the
     // flags say no edge, periodic dimensions included)
     if ((u.flags & 3) == 0) prun<K, F32, 0, false, CPL, true>(a, u, w, lane, sl);

@@ -364,14 +364,15 @@ __device__ __forceinline__ void prologue_inline(float4 (&S)[K][2], const float4*
 // stores drained, the release fence (L2 write-back), an explicit drain again (ROCm 7.2 can
 // drop the fence's own wait), then ONE lane's atomic add.
 __device__ __forceinline__ void unit_signal(unsigned long long* sig, int lane, int rel) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (the pushes are flat stores: lgkmcnt too — flat accesses complete out of order)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   // rel 0: system-scope release (L2 write-back: the RCCL path's payload lives in coarse-grained
   // tile memory another agent may read); 1: agent scope; 2: none — the direct pipeline's payload
   // was stored to the peer's UNCACHED memory, so the drained (acknowledged) stores are already
   // at their destination and only the ordering of the flag after them matters.
   if (rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   else if (rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -709,10 +710,10 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   if (xpushes != 0) {
     // side and corner pushes are complete: drain, release as the N/S signal does, then one
     // count per neighbour pushed to
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if (a.rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     else if (a.rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if (lane == 0)
       for (int i = 0; i < kSideLinks; ++i)
         if ((xpushes >> i) & 1) __hip_atomic_fetch_add(a.xsig[i], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

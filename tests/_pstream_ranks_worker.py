@@ -16,7 +16,8 @@ dist.init_process_group("gloo")
 rank = dist.get_rank()
 nx, ny, K, steps = 2 * 192 + 1, 2048, 8, 5 * 8 + 3
 e = n.Engine(nx, ny, gridx=2, gridy=1, tblock=K, device=0, ranks=[rank], transport=n.TRANSPORT_IPC,
-             halo_timeout_s=10.0, persistent=1, pstream_cols=128)
+             halo_timeout_s=10.0, persistent=1, pstream_cols=128,
+             debug_kernel=int(os.environ.get("H2D_DEBUG_KERNEL", "0")))
 # Both ranks' persistent launches share the GPU and each needs all of its waves resident: run
 # only if the two plans fit on the device together, else report a skip.
 blocks = (len(e.pstream_units(K)) + 3) // 4

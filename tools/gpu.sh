@@ -24,6 +24,7 @@ step() {  # step NAME SECONDS CMD...: run, log, stop the script on failure
 for s in "$@"; do
   case "$s" in
     tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    tests-nox3) step tests-nox3 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
     tests-nox2) step tests-nox2 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
     tests-nox) step tests-nox 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
     engine-file) step engine-file 600 python -u -m pytest tests/test_gpu_engine.py -q --timeout 300 --timeout-method thread -rf ;;
@@ -40,10 +41,7 @@ for s in "$@"; do
     convtable) step convtable 600 python -u tools/conv_table.py ;;
     pcols) step pcols 400 python -u tools/pstream_check.py cols ;;
     pphases) step pphases 300 python -u tools/pstream_check.py phases ;;
-    profconv) step profconv 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profconv -o run -- python tools/conv_probe.py 80x64 ;;
-    stress) step stress 400 python -u tools/stress_flaky.py 30 ;;
     sideweight) step sideweight 400 python -u tools/timeline.py 8192x4096:7:70 8192x4096:7:70:direct2d:side_weight=1.0 8192x4096:7:70:direct2d:side_weight=1.15 8192x4096:7:70:direct2d:side_weight=1.25 8192x4096:7:70:direct2d:side_weight=1.35 8192x4096:7:70:direct2d:side_weight=1.5 --json gpurun_out/sideweight.json ;;
-    stressseq) step stressseq 400 python -u tools/stress_seq.py 12 ;;
     pmcpst) step pmcpst 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_VALU --kernel-trace --stats -d gpurun_out/pmcpst -o run -- python tools/prof_pstream.py 512 128 ;;
     pksweep) step pksweep 300 python -u tools/pstream_check.py ksweep ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
