@@ -110,11 +110,10 @@ __device__ __forceinline__ void ppublish(unsigned* p, unsigned v, int lane) {
   if (lane == 0) __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The direct pipeline's flag signal of a halo unit.  The pushes are flat stores (the peer's
-// IPC-mapped buffer), which complete out of order with the counted vmcnt of the publishing top:
-// drain them (vmcnt and lgkmcnt) before the flag, whatever the release flavour.
+// The direct pipeline's flag signal of a halo unit (its pushed rows' stores have completed: the
+// pushes are global stores, in issue order with the row stores the publishing top's counted
+// vmcnt covers).
 __device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int lane) {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   else if (rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   if (rel != 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

@@ -187,30 +187,40 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // objects).  Under memory load the store then writes the new value for some lanes — measured:
 // element 1 of lanes 12-15 of every 16 in one row per unit (2-step 257x509 run), and the
 // intermittent wrong tiles of round 3 (the residual launches convert each stored row to fp64 in
-// place).  Every wide store is followed by `s_nop 1` that reads its data registers, so they stay
-// unchanged until two wait states after the store (the lint checks the built code objects).
+// place).  hipcc does pad the same store with an immediate soffset, so the write-through row
+// stores carry the row offset in the vector offset (soffset 0) and need nothing more; every other wide store is followed by `s_nop 1` that reads its data
+// registers, ordered after the store by its memory clobber (tools/hazard_lint.py checks every
+// built code object for the pattern).
 __device__ __forceinline__ void store_guard(const u32x4& d) { asm volatile("s_nop 1" ::"v"(d) : "memory"); }
 
 __device__ __forceinline__ u32x4 as_u32x4(const float4& o) {
   return u32x4{__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(o.w)};
 }
 
-// Plain wide store of a lane's cells (16 B guarded; 8 B needs no guard).
+// Plain wide store of a lane's cells (16 B guarded; 8 B needs no guard).  Global address space
+// (global_store, not flat_store): it completes in issue order with the buffer loads and stores,
+// so the counted `s_waitcnt vmcnt(N)` of the persistent kernel covers it (flat accesses complete
+// out of order).
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u32x2_ gu32x2;
 __device__ __forceinline__ void store_cells(float* p, const float4& o) {
   const u32x4 d = as_u32x4(o);
-  *reinterpret_cast<u32x4*>(p) = d;
+  *(gu32x4*)p = d;
   store_guard(d);
 }
-__device__ __forceinline__ void store_cells(float* p, const float2& o) { *reinterpret_cast<float2*>(p) = o; }
+__device__ __forceinline__ void store_cells(float* p, const float2& o) {
+  *(gu32x2*)p = u32x2_{__float_as_uint(o.x), __float_as_uint(o.y)};
+}
 
 // Store one lane's float4 of an output row write-through (buffer_store_dwordx4 ... sc1):
 // 16-B sc1 stores cost about a plain store, and leave no dirty line in the L2.  The resource is
-// loop-invariant (the unit's base); the row moves through the scalar offset.
+// loop-invariant (the unit's base); the row's byte offset is added to the lane's vector offset
+// (soffset 0, see the hazard note above).  A dropped lane's offset starts at 2^31 and a row
+// offset stays below 2^31 (the host's limit), so it never wraps back into the record range.
 __device__ __forceinline__ void store_row_wt(float* base, unsigned voff, int soff, const float4& o) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-  const u32x4 d = as_u32x4(o);
-  __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)voff, soff, 16 /* sc1 */);
-  store_guard(d);
+  __builtin_amdgcn_raw_buffer_store_b128(as_u32x4(o), r, (int)(voff + (unsigned)soff), 0, 16 /* sc1 */);
 }
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -532,6 +542,12 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
       return;
     }
   }
+  // replay check: launch ids rise in stream order, so an older or equal id seen already means this
+  // launch ran with the arguments of an earlier one.  Issued here, its value is checked at the
+  // wave's end (the atomic's round trip overlaps the work instead of delaying the launch's end).
+  unsigned long long lid_old = 0ull;
+  const bool replay_check = w == 0 && lane == 0 && a.lid != 0ull && a.lid_seen != nullptr;
+  if (replay_check) lid_old = __hip_atomic_fetch_max(a.lid_seen, a.lid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool halo_unit = w < a.nsignal;
   const bool ns_unit = halo_unit && (u.flags & kUnitNS) != 0;  // top / bottom halo unit of its strip
   const int dir = (u.flags & kUnitReverse) ? 1 : 0;  // 0: north halo (top unit), 1: south (bottom unit)
@@ -724,12 +740,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     if (slot >= a.nunits) slot -= a.nunits;
     publish_partial(a.partials, slot, racc, a.nunits, a.dec, lane);
   }
-  if (w == 0 && lane == 0 && a.lid != 0ull && a.lid_seen != nullptr) {
-    // replay check: launch ids rise in stream order, so an older or equal id seen already means
-    // this launch ran with the arguments of an earlier one
-    if (__hip_atomic_fetch_max(a.lid_seen, a.lid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.lid)
-      report_timeout(a.timed_out, a.timed_out_host, kIntegReplay);
-  }
+  if (replay_check && lid_old >= a.lid) report_timeout(a.timed_out, a.timed_out_host, kIntegReplay);
   if (stamping) {
     // the wave's stores have drained: its work is done, not just issued
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

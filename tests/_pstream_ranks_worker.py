@@ -39,12 +39,27 @@ e.run(steps)
 e.synchronize()
 g = e.geom(0)
 ref = n.oracle_run(nx, ny, steps)["grid"][g["gx0"]:g["gx0"] + g["xcell"], :]
-ok = bool(np.array_equal(e.download(0), ref))
+got = e.download(0)
+ok = bool(np.array_equal(got, ref))
+
+
+def where(got, ref):
+    bad = got != ref
+    if not bad.any():
+        return None
+    r, c = np.nonzero(bad)
+    return [int(bad.sum()), int(r.min()), int(r.max()), int(c.min()), int(c.max()), sorted(set(r.tolist()))[:12]]
+
+
+bad1 = where(got, ref)
 dist.barrier()
 e.run(2 * K)
 e.synchronize()
 ref2 = n.oracle_run(nx, ny, steps + 2 * K)["grid"][g["gx0"]:g["gx0"] + g["xcell"], :]
-ok2 = bool(np.array_equal(e.download(0), ref2))
+got2 = e.download(0)
+ok2 = bool(np.array_equal(got2, ref2))
 print(json.dumps({"rank": rank, "ok": ok, "ok2": ok2, "launches": e.pstream_launches()}), flush=True)
+if not (ok and ok2):
+    print(f"rank {rank} xcell {g['xcell']}: first run wrong {bad1}; second {where(got2, ref2)}", flush=True)
 dist.barrier()
 dist.destroy_process_group()

@@ -7,7 +7,7 @@ pad such a write when it was a packed-FP32 VALU op (`v_pk_add_f32` right after a
 `buffer_store_dwordx4`): lanes of the stored row came out wrong under memory load, intermittently.
 
 This lint disassembles every device code object of the build (build/obj/*.o, .hip_fatbin) and
-reports each wide store followed, within 2 wait states, by an instruction that writes one of
+reports each wide store followed, within 2 wait states, by a VALU instruction that writes one of
 its data VGPRs.  Usage: python tools/hazard_lint.py [objects...]  (exit 1 on a finding).
 """
 from __future__ import annotations
@@ -64,8 +64,9 @@ def findings(ins: list) -> list:
             if q[0] == "s_nop":
                 ws += int(q[1], 0) + 1
             else:
-                if len(q) > 1 and q[0].startswith(("v_", "global_load", "buffer_load", "ds_read", "flat_load")) \
-                        and vregs(q[1]) & data:
+                # VALU writers only: a vector-memory load issues behind the store in the same memory
+                # pipeline and returns its data hundreds of cycles later
+                if len(q) > 1 and q[0].startswith("v_") and vregs(q[1]) & data:
                     bad.append((ws, l, ins[j]))
                     break
                 ws += 1
