@@ -1620,6 +1620,12 @@ void Engine::launch_pstream_chunks(int K, int J) {
     }
     a.ipar0 = (int)(ipc_chunk_ & 1);
     a.sig_rows = G_;
+    for (int d = 0; d < 2; ++d) {  // chunk order of my halo units' signals (PStreamArgs::lsig)
+      a.lsig[d] = reinterpret_cast<unsigned long long*>(ipc_block_ + me.lsig[d]);
+      a.lbase[d] = ipc_lsig_[d];
+      a.lper[d] = P.pushes[d];
+      ipc_lsig_[d] += (unsigned long long)J * (unsigned long long)P.pushes[d];
+    }
     a.rel = opt_.direct_release < 0 ? 2 : opt_.direct_release;
     a.acq = opt_.direct_acquire < 0 ? 1 : opt_.direct_acquire;
   }
@@ -2018,7 +2024,7 @@ Engine::IpcLayout Engine::ipc_layout_of(int rank) const {
     off += (((size_t)(g.xcell + 2 * g.G) * (size_t)g.pitch * sizeof(float)) + 4095) & ~size_t(4095);
   }
   L.bytes = off;
-  static_assert(1152 + 2 * kIpcMaxRanks * sizeof(double) <= 4096, "IPC residual slots overflow the header");
+  static_assert(1152 + 2 * kIpcMaxRanks * sizeof(double) <= 2304, "IPC residual slots overflow into the signal counters");
   return L;
 }
 
@@ -2148,6 +2154,7 @@ void Engine::ipc_prime() {
   H2D_HIP_CHECK(hipDeviceSynchronize());
   ipc_chunk_ = 0;
   for (auto& v : ipc_need_) v = 0;
+  for (auto& v : ipc_lsig_) v = 0;
   ipc_resid_epoch_ = 0;
   ipc_primed_ = true;
 }

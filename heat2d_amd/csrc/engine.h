@@ -375,6 +375,7 @@ class Engine {
   struct IpcLayout {
     size_t flag[kNumDirs] = {};                   // pushes arrived from the neighbour in direction d
     size_t resid_count = 1024, resid_slots = 1152;  // byte offsets
+    size_t lsig[2] = {2304, 2432};  // my N / S halo units' signals of persistent launches (chunk order)
     size_t recv_n[2] = {0, 0}, recv_s[2] = {0, 0};
     size_t xbuf = 0;     // W / E ghost-column groups (2-D blocks only; 0: none)
     int64_t pitch = 0;   // the tile's row pitch (floats): also the xbuf's
@@ -398,6 +399,7 @@ class Engine {
   bool ipc_primed_ = false;
   unsigned long long ipc_chunk_ = 0;        // chunks since the prime (receive-buffer parity)
   unsigned long long ipc_need_[kNumDirs] = {};  // halo pushes expected from each direction (cumulative)
+  unsigned long long ipc_lsig_[2] = {};         // my persistent N / S signals so far (IpcLayout::lsig)
   unsigned long long ipc_resid_epoch_ = 0;  // residual all-reduces since the prime
   // ---- persistent pipelined stencil ----
   struct PPlan {

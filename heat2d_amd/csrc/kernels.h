@@ -240,6 +240,14 @@ struct PStreamArgs {
   // and receive-buffer parity: chunk j reads parity (ipar0 + j) & 1 and pushes to the other
   const unsigned long long* wait[2] = {nullptr, nullptr};
   unsigned long long need0[2] = {0, 0}, need_inc[2] = {0, 0};
+  // chunk order of the signals: a halo unit signals chunk j of the launch only once all of this
+  // rank's halo units of its direction have signalled chunk j-1 (*lsig[d] counts them, lbase[d]
+  // before the launch, lper[d] per chunk).  The neighbour's wait counts pushes summed over ALL
+  // strips, so without it a strip running a chunk ahead could stand in for a slow strip's missing
+  // push and the neighbour would read that strip's ghost rows before they landed.
+  unsigned long long* lsig[2] = {nullptr, nullptr};
+  unsigned long long lbase[2] = {0, 0};
+  int lper[2] = {0, 0};
   const float* hsrc[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   float* push[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   unsigned long long* sig[2] = {nullptr, nullptr};

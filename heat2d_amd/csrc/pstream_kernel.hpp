@@ -110,14 +110,30 @@ __device__ __forceinline__ void ppublish(unsigned* p, unsigned v, int lane) {
   if (lane == 0) __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The direct pipeline's flag signal of a halo unit (its pushed rows' stores have completed: the
-// pushes are global stores, in issue order with the row stores the publishing top's counted
-// vmcnt covers).
-__device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int lane) {
+// The direct pipeline's flag signal of a halo unit for chunk `jc` of the launch (its pushed rows'
+// stores have completed: the pushes are global stores, in issue order with the row stores the
+// publishing top's counted vmcnt covers).  First, bounded, every halo unit of this rank and
+// direction must have signalled chunk jc-1 (PStreamArgs::lsig): the neighbour's flag then only
+// ever counts whole chunks.
+__device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int lane, unsigned long long* lsig,
+                                        unsigned long long lneed, const PStreamArgs& a, bool& dead) {
+  if (lsig != nullptr && lane == 0 && !dead) {
+    long long i = 0;
+    while (__hip_atomic_load(lsig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < lneed) {
+      if (++i > a.halo_polls) {
+        report_timeout(a.timed_out, a.timed_out_host, 8u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
   if (rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   else if (rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   if (rel != 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) {
+    __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lsig != nullptr) __hip_atomic_fetch_add(lsig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // PUSH: a direct-pipeline halo unit (copies its first rows to the neighbour GPU each chunk); the
@@ -191,6 +207,9 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   float* const push0 = rev ? a.push[1][0] : a.push[0][0];
   float* const push1 = rev ? a.push[1][1] : a.push[0][1];
   unsigned long long* const sigd = rev ? a.sig[1] : a.sig[0];
+  unsigned long long* const lsigd = rev ? a.lsig[1] : a.lsig[0];
+  const unsigned long long lbased = rev ? a.lbase[1] : a.lbase[0];
+  const unsigned long long lperd = (unsigned long long)(rev ? a.lper[1] : a.lper[0]);
   const bool pushes = PUSH && ns && push0 != nullptr;
   c.prows = pushes ? a.sig_rows : 0;
   const int64_t in_base = (a.G + x0 - K) * a.pitch + a.PL + u.cb;  // lowest input row, lane 0
@@ -202,6 +221,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
 
   bool dead = false;         // a wait gave up: finish without waiting (the host reports it)
   bool sig_pending = false;  // a halo unit's pushes of its last chunk are not yet signalled
+  int sig_chunk = 0;         // ... of that chunk
   double racc = 0.0;
   // diagnostics: per-phase time of this wave, compiled in only with -DH2D_PSTREAM_PHASES (even
   // an untaken runtime branch per iteration top cost ~30 % at 512x4096: the timers' registers
@@ -234,7 +254,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       ppublish(myprog, cidx * (unsigned)h, lane);
       if (sig_pending) {
-        psignal(sigd, a.rel, lane);
+        psignal(sigd, a.rel, lane, lsigd, lbased + (unsigned long long)sig_chunk * lperd, a, dead);
         sig_pending = false;
       }
       sl.known = max(sl.known, pv);
@@ -312,7 +332,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);
         if (pushes && !signalled && issued_prev >= a.sig_rows) {  // the pushed rows have completed
-          psignal(sigd, a.rel, lane);
+          psignal(sigd, a.rel, lane, lsigd, lbased + (unsigned long long)j * lperd, a, dead);
           signalled = true;
         }
         if (have_poll) sl.known = max(sl.known, polled);
@@ -345,12 +365,15 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
     }
     if (have_poll) sl.known = max(sl.known, polled);
     // pushes not yet signalled at an iteration top: at the next chunk start (or launch end)
-    if (pushes && !signalled) sig_pending = true;
+    if (pushes && !signalled) {
+      sig_pending = true;
+      sig_chunk = j;
+    }
   }
   lap(5);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   ppublish(myprog, (a.cbase + (unsigned)a.nchunks) * (unsigned)h, lane);
-  if (sig_pending) psignal(sigd, a.rel, lane);
+  if (sig_pending) psignal(sigd, a.rel, lane, lsigd, lbased + (unsigned long long)sig_chunk * lperd, a, dead);
   lap(1);
 #ifdef H2D_PSTREAM_PHASES
   if (tm && lane == 0) {
