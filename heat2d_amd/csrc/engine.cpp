@@ -1621,7 +1621,8 @@ void Engine::launch_pstream_chunks(int K, int J) {
     a.ipar0 = (int)(ipc_chunk_ & 1);
     a.sig_rows = G_;
     for (int d = 0; d < 2; ++d) {  // chunk order of my halo units' signals (PStreamArgs::lsig)
-      a.lsig[d] = reinterpret_cast<unsigned long long*>(ipc_block_ + me.lsig[d]);
+      // (debug_kernel bit 4: without the chunk order — diagnostics only, races between processes)
+      a.lsig[d] = (opt_.debug_kernel & 4) ? nullptr : reinterpret_cast<unsigned long long*>(ipc_block_ + me.lsig[d]);
       a.lbase[d] = ipc_lsig_[d];
       a.lper[d] = P.pushes[d];
       ipc_lsig_[d] += (unsigned long long)J * (unsigned long long)P.pushes[d];

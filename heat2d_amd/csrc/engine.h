@@ -106,7 +106,8 @@ struct EngineOptions {
   // streaming launches of each run (0: off).  Read back with Engine::timeline().
   int timeline = 0;
   bool poison = false;        // debug canary: NaN in every cell no valid update may read
-  // diagnostics: 1 every streaming unit runs the halo-unit bodies; 2 no integrity checks (launch id 0)
+  // diagnostics: 1 every streaming unit runs the halo-unit bodies; 2 no integrity checks (launch id 0);
+  // 4 persistent halo signals without their chunk order (unsafe between processes)
   int debug_kernel = 0;
   bool convergence = false;
   int64_t interval = 20;
