@@ -180,9 +180,10 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
     }
     d_wait_acc_ = dmalloc<unsigned long long>(4);
     dzero(d_wait_acc_, 4 * sizeof(unsigned long long));
-    d_lid_seen_ = dmalloc<unsigned long long>(2);
-    dzero(d_lid_seen_, 2 * sizeof(unsigned long long));
+    d_lid_seen_ = dmalloc<unsigned long long>(3);
+    dzero(d_lid_seen_, 3 * sizeof(unsigned long long));
     d_copies_done_ = d_lid_seen_ + 1;
+    d_waves_done_ = d_lid_seen_ + 2;
     if (o.timeline > 0) {
       if (o.timeline > 4096) throw std::invalid_argument("timeline: at most 4096 launches");
       d_stamps_ = dmalloc<unsigned long long>((size_t)o.timeline * kTimelineUnits * 4);
@@ -654,6 +655,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     // serial local pipeline: the exchange copies in front of this launch on the compute stream
     a.copies_done = d_copies_done_;
     a.copies_need = copies_need_;
+    a.waves_done = d_waves_done_;
   }
   if (which == 0) {
     a.units = L.d_all;
@@ -738,6 +740,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     tl_recs_.emplace_back(K, a.nunits);
   }
   launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
+  if (a.waves_done != nullptr) waves_need_ += (unsigned long long)a.nunits;
   progress_tick(stream ? stream : compute_);
   if (residual && whole && !lone) reduce_tile_residual(t, K);
   if (residual && whole && lone) {
@@ -853,7 +856,8 @@ void Engine::local_copy(const DescList& D, hipStream_t s) {
   // on the compute stream the copy blocks are counted: the serial pipeline's stencil launch
   // checks that all of them completed before it started (kIntegOrder)
   const bool counted = s == compute_;
-  launch_copy_rects(D.d, D.n, D.maxe, s, D.tag, counted ? d_copies_done_ : nullptr, d_sig_timeout_, h_timeout_dev_);
+  launch_copy_rects(D.d, D.n, D.maxe, s, D.tag, counted ? d_copies_done_ : nullptr, d_sig_timeout_, h_timeout_dev_,
+                    counted ? d_waves_done_ : nullptr, waves_need_);
   if (counted) copies_need_ += (unsigned long long)copy_rects_blocks(D.n, D.maxe);
 }
 
@@ -1110,14 +1114,15 @@ void Engine::poll_abort() {
   unsigned int all = to;
   if (hipMemcpy(&all, d_sig_timeout_, sizeof(all), hipMemcpyDeviceToHost) != hipSuccess) all = to;
   all |= to;
-  const unsigned integ = kIntegArgs | kIntegUnits | kIntegReplay | kIntegDescs | kIntegOrder;
+  const unsigned integ = kIntegArgs | kIntegUnits | kIntegReplay | kIntegDescs | kIntegOrder | kIntegOrder2;
   if (all & integ) {
     broken_why_ = std::string("integrity check failed (bits ") + std::to_string(all) + "): " +
                   ((all & kIntegArgs) ? "torn kernel arguments (launch ids at the two ends differ) " : "") +
                   ((all & kIntegUnits) ? "a work unit of another list (stale unit-list upload) " : "") +
                   ((all & kIntegReplay) ? "a launch ran with the arguments of an earlier launch " : "") +
                   ((all & kIntegDescs) ? "a copy descriptor of another list (stale descriptor upload) " : "") +
-                  ((all & kIntegOrder) ? "a stencil launch started before its exchange copy finished " : "");
+                  ((all & kIntegOrder) ? "a stencil launch started before its exchange copy finished " : "") +
+                  ((all & kIntegOrder2) ? "an exchange copy started before the stencil launches before it finished " : "");
   } else {
     broken_why_ = std::string("signalled halo pipeline timed out: ") +
                   ((all & 1) ? "the exchange gate (boundary units never completed) " : "") +

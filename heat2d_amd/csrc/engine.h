@@ -341,6 +341,8 @@ class Engine {
   unsigned long long* d_lid_seen_ = nullptr;    // highest launch id a launch has completed
   unsigned long long* d_copies_done_ = nullptr;  // local exchange copy blocks completed (compute stream)
   unsigned long long copies_need_ = 0;          // ... enqueued
+  unsigned long long* d_waves_done_ = nullptr;  // serial pipeline: stencil waves completed
+  unsigned long long waves_need_ = 0;           // ... enqueued
   static int next_tag();                        // process-wide plan tags (never 0)
   unsigned long long* d_wait_acc_ = nullptr;  // StreamArgs::wait_acc (3 words)
   unsigned long long* d_stamps_ = nullptr;    // StreamArgs::stamps ring (timeline diagnostics)

@@ -112,6 +112,7 @@ constexpr unsigned kIntegUnits = 32u;    // a unit's tag is not the tag of the l
 constexpr unsigned kIntegReplay = 64u;   // a launch ran with the arguments of an earlier launch
 constexpr unsigned kIntegDescs = 128u;   // a copy descriptor's tag is not the list's tag
 constexpr unsigned kIntegOrder = 256u;   // a stencil launch started before its exchange copy finished
+constexpr unsigned kIntegOrder2 = 512u;  // an exchange copy started before the stencil launches before it finished
 
 // Arguments of the temporally-blocked streaming stencil.
 struct StreamArgs {
@@ -200,6 +201,7 @@ struct StreamArgs {
   unsigned long long* lid_seen = nullptr;
   const unsigned long long* copies_done = nullptr;
   unsigned long long copies_need = 0;
+  unsigned long long* waves_done = nullptr;  // serial pipeline: every wave adds 1 at its end (its stores drained)
   unsigned long long lid_tail = 0;
 };
 
@@ -294,9 +296,12 @@ void launch_poison(const TileGeom& g, float* base, bool fixed, bool per_x, bool 
 // tag != 0: every descriptor must carry it (else kIntegDescs is reported through integ /
 // integ_host and the block copies nothing); done != nullptr: each block adds 1 when its copies
 // are issued and drained (the serial pipeline's ordering check, StreamArgs::copies_done).
+// waves_done != nullptr: block (0, 0) checks that it equals waves_need (every stencil wave
+// enqueued before the copy has finished: kIntegOrder2).
 void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s, int64_t tag = 0,
                        unsigned long long* done = nullptr, unsigned int* integ = nullptr,
-                       unsigned int* integ_host = nullptr);
+                       unsigned int* integ_host = nullptr, const unsigned long long* waves_done = nullptr,
+                       unsigned long long waves_need = 0);
 // blocks launch_copy_rects uses for (ndesc, max_elems): what a `done` counter advances by
 int64_t copy_rects_blocks(int ndesc, int64_t max_elems);
 void launch_reduce_sum(const double* in, int n, double* out, hipStream_t s);

@@ -49,8 +49,12 @@ __global__ void poison_kernel(TileGeom g, float* __restrict__ base, int fixed, i
 }
 
 __global__ void copy_rects_kernel(const CopyDesc* __restrict__ descs, int64_t tag, unsigned long long* done,
-                                  unsigned int* integ, unsigned int* integ_host) {
+                                  unsigned int* integ, unsigned int* integ_host, const unsigned long long* waves_done,
+                                  unsigned long long waves_need) {
   const CopyDesc d = descs[blockIdx.y];
+  if (waves_done != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 &&
+      __hip_atomic_load(waves_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != waves_need)
+    report_timeout(integ, integ_host, kIntegOrder2);
   if (tag != 0 && d.tag != tag) {
     // a descriptor of another list (stale upload / reused allocation): copy nothing, report
     if (threadIdx.x == 0) report_timeout(integ, integ_host, kIntegDescs);
@@ -739,11 +743,12 @@ int64_t copy_rects_blocks(int ndesc, int64_t max_elems) {
 }
 
 void launch_copy_rects(const CopyDesc* d_descs, int ndesc, int64_t max_elems, hipStream_t s, int64_t tag,
-                       unsigned long long* done, unsigned int* integ, unsigned int* integ_host) {
+                       unsigned long long* done, unsigned int* integ, unsigned int* integ_host,
+                       const unsigned long long* waves_done, unsigned long long waves_need) {
   if (ndesc <= 0 || max_elems <= 0) return;
   const unsigned bx = (unsigned)std::min<int64_t>((max_elems + 255) / 256, 1024);
   hipLaunchKernelGGL(copy_rects_kernel, dim3(bx, (unsigned)ndesc), dim3(256), 0, s, d_descs, tag, done, integ,
-                     integ_host);
+                     integ_host, waves_done, waves_need);
   H2D_HIP_CHECK(hipGetLastError());
 }
 

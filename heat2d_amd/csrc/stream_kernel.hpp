@@ -539,6 +539,8 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
       bad = kIntegOrder;
     if (bad != 0u) {
       if (lane == 0) report_timeout(a.timed_out, a.timed_out_host, bad);
+      if (lane == 0 && a.waves_done != nullptr)
+        __hip_atomic_fetch_add(a.waves_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
   }
@@ -561,6 +563,8 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     if (lane == 0)
       for (int i = 0; i < kSideLinks; ++i)
         if ((xpushes >> i) & 1) __hip_atomic_fetch_add(a.xsig[i], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0 && a.waves_done != nullptr)
+      __hip_atomic_fetch_add(a.waves_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   const bool ns_wait = ns_unit && a.wait[dir] != nullptr;
@@ -741,6 +745,12 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     publish_partial(a.partials, slot, racc, a.nunits, a.dec, lane);
   }
   if (replay_check && lid_old >= a.lid) report_timeout(a.timed_out, a.timed_out_host, kIntegReplay);
+  if (a.waves_done != nullptr) {
+    // serial pipeline: this wave's stores are complete — the next exchange copy checks that every
+    // wave of the launches before it got here
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(a.waves_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (stamping) {
     // the wave's stores have drained: its work is done, not just issued
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
