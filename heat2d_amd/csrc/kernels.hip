@@ -60,13 +60,14 @@ __global__ void copy_rects_kernel(const CopyDesc* __restrict__ descs, int64_t ta
     if (threadIdx.x == 0) report_timeout(integ, integ_host, kIntegDescs);
   } else {
     const int64_t total = d.rows * d.cols;
-    // write-through stores (agent-scope atomic store = global_store ... sc1), like the stencil's
-    // outputs: no dirty line of a ghost row stays in this XCD's L2 for the next launch of the
-    // stream (a consumer on another XCD) to miss
+    // agent-coherent loads and write-through stores (agent-scope atomics = global_load / store
+    // ... sc1), like the stencil's outputs: no dirty line of a ghost row stays in this XCD's L2,
+    // and no stale line of the peer's edge rows is read from it
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
       const int64_t r = e / d.cols, cc = e - r * d.cols;
-      __hip_atomic_store(d.dst + r * d.dst_pitch + cc, d.src[r * d.src_pitch + cc], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.dst + r * d.dst_pitch + cc,
+                         __hip_atomic_load(d.src + r * d.src_pitch + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (done != nullptr) {
