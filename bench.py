@@ -313,6 +313,9 @@ def main() -> int:
                          "note": "worst rank; in-kernel flag-poll time of the halo units during the timed runs "
                                  "(Report.pdf p.34-37 MPI_Waitall analogue)"}
 
+    # persistent launches per rank over the whole job (0: one launch per chunk)
+    plaunches = ctx.gather_objects(int(s.engine.pstream_launches()))
+
     # ---- in-job single-GPU reference: speedup / efficiency, and bit-exact verification ------
     t1 = None
     verified_full = None
@@ -414,6 +417,7 @@ def main() -> int:
                 "candidate": f"{transport}/{pipeline}",
                 "tblock": halo_depth,
                 "path": path,
+                "persistent_launches_per_rank": plaunches,
                 "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             },
         }

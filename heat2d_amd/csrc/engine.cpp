@@ -1540,7 +1540,8 @@ const Engine::PPlan* Engine::pplan(int K) {
     // the K-cone (K-1)/h halves), else 256 (profiles/pstream_r3.txt, us/step 256 vs 128 columns,
     // K=8: 512x4096 2.077 vs 1.908; 1024 rows 2.867 vs 3.031; 2048 rows 4.789 vs 5.157)
     P.cpl = opt_.pstream_cols == 256 ? 4 : opt_.pstream_cols == 128 ? 2 : (g.xcell <= 768 ? 2 : 4);
-    const int64_t cap = (int64_t)device_cus_ * 4;  // one wave per SIMD, every wave resident
+    int64_t cap = (int64_t)device_cus_ * 4;  // one wave per SIMD, every wave resident
+    if (opt_.pstream_waves > 0) cap = std::min<int64_t>(cap, opt_.pstream_waves);
     const int bpc = pstream_blocks_per_cu(K, opt_.precision, P.cpl);
     P.host = plan_pstream(g, K, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                           opt_.row_edge_weight > 0 ? opt_.row_edge_weight : opt_.edge_weight, cap, halo_n, halo_s,

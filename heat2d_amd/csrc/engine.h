@@ -96,6 +96,9 @@ struct EngineOptions {
   // Strip width of the persistent kernel: 256 (4 columns per lane), 128 (2 per lane: units twice
   // as tall for the same wave count, so a short tile's K-cone costs half as much), 0 auto.
   int pstream_cols = 0;
+  // Waves of one persistent launch at most (0: one per SIMD of the device).  Ranks that share a
+  // GPU (a one-GPU rehearsal of an N-GPU run) split it, so every rank's waves are resident at once.
+  int pstream_waves = 0;
   // 2-D direct pipeline: cost weight per row of the units that push to a W / E neighbour
   double side_weight = 1.35;
   // Diagnostics: per-phase timers of the persistent kernel (PStreamArgs::phase)

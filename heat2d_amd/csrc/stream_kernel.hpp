@@ -422,21 +422,35 @@ __device__ __forceinline__ void run_unit(const float4* __restrict__ rowp, const 
 #endif
 
   int ir0 = 2 * K;  // even: slot parity of sub-step d is d & 1
-#define H2D_STEADY(D)                                                        \
-  {                                                                          \
-    const float4 nw = pf[D];                                                 \
-    pf[D] = rowp[(int64_t)min(ir0 + (D) + 4, n - 1) * pitch4];               \
-    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
+  // The next four rows are loaded at the top of each 4-row half, a whole half ahead of their use,
+  // into the register set the previous half consumed (ping-pong: no register copies, whose waits
+  // the compiler placed as vmcnt(0) — a drain of the write-through row stores too).  Left to the
+  // scheduler, the straight-line body issued the loads late and waited the same way (+3 %).
+#define H2D_HALF(CUR, NXT, R0)                                                             \
+  {                                                                                        \
+    if constexpr (HALO)                                                                    \
+      if ((R0) == sig_at) unit_signal(sig, lane, c.rel);                                   \
+    _Pragma("unroll") for (int d = 0; d < 4; ++d)                                          \
+        NXT[d] = rowp[(int64_t)min((R0) + d + 4, n - 1) * pitch4];                         \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 0, K>(S, CUR[0], (R0) + 0, c, k, racc); \
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 1, K>(S, CUR[1], (R0) + 1, c, k, racc); \
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 0, K>(S, CUR[2], (R0) + 2, c, k, racc); \
+    process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 1, K>(S, CUR[3], (R0) + 3, c, k, racc); \
+  }
+  float4 nx[4];
+  if constexpr (K <= 8) {  // deeper variants (off the bench's path) keep half the code: build time
+    for (; ir0 + 8 <= n; ir0 += 8) {
+      H2D_HALF(pf, nx, ir0)
+      H2D_HALF(nx, pf, ir0 + 4)
+    }
   }
   for (; ir0 + 4 <= n; ir0 += 4) {
-    if constexpr (HALO)
-      if (ir0 == sig_at) unit_signal(sig, lane, c.rel);
-    H2D_STEADY(0)
-    H2D_STEADY(1)
-    H2D_STEADY(2)
-    H2D_STEADY(3)
+    H2D_HALF(pf, nx, ir0)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) pf[d] = nx[d];
   }
-#undef H2D_STEADY
+#undef H2D_HALF
   // tail: at most 3 rows
   if (ir0 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 0, K>(S, pf[0], ir0, c, k, racc);
   if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, RESID, WT, SIDE, HALO, 1, K>(S, pf[1], ir0 + 1, c, k, racc);

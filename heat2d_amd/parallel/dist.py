@@ -151,6 +151,7 @@ class DistContext:
         explicitly, or see one GPU each under different numbering.  Sets ``distinct_devices``."""
         if not self.is_multi:
             self.distinct_devices = device >= 0
+            self.ranks_on_device = 1
             return False
         import socket
 
@@ -158,6 +159,8 @@ class DistContext:
         ids = self.all_gather_bytes(ident.encode())
         shared = device >= 0 and len(set(ids)) < len(ids)
         self.distinct_devices = device >= 0 and not shared
+        # ranks on this rank's GPU (itself included)
+        self.ranks_on_device = sum(1 for i in ids if i == ident.encode()) if device >= 0 else 1
         return shared
 
     def get_nccl_group(self):

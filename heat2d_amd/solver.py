@@ -211,6 +211,11 @@ class Solver:
             raise ValueError(f"unknown persistent mode {cfg.persistent!r}")
         if cfg.persistent != "auto":
             kw["persistent"] = 1 if cfg.persistent == "on" else 0
+            share = getattr(self.ctx, "ranks_on_device", 1) if getattr(self, "shared_gpu", False) else 1
+            if cfg.persistent == "on" and share > 1:
+                # a one-GPU rehearsal: the ranks on this GPU split its wave slots, so each rank's
+                # persistent launch is resident beside the others'
+                kw["pstream_waves"] = 4 * n.device_props(self.device)["multiprocessor_count"] // share
         elif getattr(self, "shared_gpu", False):
             # ranks share a GPU: a persistent launch needs every one of its waves resident, which
             # another rank's persistent launch on the same GPU could prevent — launch per chunk

@@ -4,6 +4,8 @@ Every result in the ``ref`` precision must be bit-identical to ``oracle_run`` (t
 reference semantics); fp32 results must be bit-identical to the CPU engine's fp32 path
 (both use fused multiply-adds) and within tolerance of a plain PyTorch fp32 stencil.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -508,7 +510,10 @@ def _outside_nonzero(eng, t, b):
 # new engine's run compute wrong tiles, and once fault with an illegal memory access that poisoned
 # every later test of the process (docs/ARCHITECTURE.md, Known issues); in a fresh process it never
 # failed (tools/serial_repro.py create-first).
-@pytest.mark.parametrize("order", ["release-first"])
+_SERIAL_ORDERS = ["release-first"] + [o for o in os.environ.get("H2D_SERIAL_ORDERS", "").split(",") if o]
+
+
+@pytest.mark.parametrize("order", _SERIAL_ORDERS)
 @pytest.mark.parametrize("gx,gy", [(2, 1), (1, 2)])
 def test_serial_tiles_long_convergence_run(native, gpu, gx, gy, order):
     """The local two-tile serial pipeline with checks every 9 steps, as ONE run of up to 3000 steps
@@ -518,9 +523,12 @@ def test_serial_tiles_long_convergence_run(native, gpu, gx, gy, order):
     nx, ny = 257, 509
     ref = oracle(native, nx, ny, 3000, 1, **CONV)
     eng = None
+    kept = []
     for fused in (-1, 0):
         if order == "release-first":
             eng = None  # the previous engine is released before the next one is built
+        elif order == "create-keep":
+            kept.append(eng)  # the previous engine stays alive through the next run
         eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
                             small_grid_lds=False, tiled=0, overlap=False, **CONV)
         st = eng.run(3000)

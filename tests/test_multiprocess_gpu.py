@@ -110,6 +110,22 @@ def test_gpu_bench_four_ranks_blocks_ipc(tmp_path):
     assert min(d["halo_wait"]["waits_per_rank"]) > 0
 
 
+@pytest.mark.parametrize("n", [4, 8])
+def test_gpu_bench_persistent_rehearsal(tmp_path, n):
+    """The driver's N=4 / N=8 strong-scaling command (4096^2, row strips) with every rank on one
+    GPU and the persistent kernel forced on: the ranks split the GPU's wave slots
+    (pstream_waves), every rank runs persistent launches through the direct pipeline, and the
+    timed result is bit-exact (CPU oracle on the leading steps, rank 0's single-GPU run after all
+    of them)."""
+    out = _torchrun(n, [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "42", "--warmup", "14",
+                        "--persistent", "on", "--prewarm-s", "0"], str(tmp_path))
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert d["config"]["parallelism"] == f"rows{n}" and d["config"]["grid_per_gpu"] == [4096 // n, 4096]
+    assert d["config"]["pipeline"] == "direct" and d["verified"] is True
+    pl = d["config"]["persistent_launches_per_rank"]
+    assert len(pl) == n and min(pl) > 0, pl
+
+
 def test_gpu_bench_two_ranks_ipc(tmp_path):
     """The bench at N=2 on one GPU: the gate picks the direct IPC transport first."""
     out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "40", "--warmup", "8", "--side",

@@ -24,26 +24,15 @@ step() {  # step NAME SECONDS CMD...: run, log, stop the script on failure
 for s in "$@"; do
   case "$s" in
     tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
-    tests-nox3) step tests-nox3 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
-    tests-nox2) step tests-nox2 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
-    tests-nox) step tests-nox 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
+    tests-nox) step tests-nox 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf ;;
     engine-file) step engine-file 600 python -u -m pytest tests/test_gpu_engine.py -q --timeout 300 --timeout-method thread -rf ;;
+    serial) step serial 600 python -u -m pytest tests/test_gpu_engine.py -v --timeout 300 --timeout-method thread -rf -k serial_tiles_long ;;
     tests-k) step tests-k 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf -k "$TESTK" ;;
-    tests-new) step tests-new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-                 tests/test_gpu_engine.py -k "bench_shape or rank_tiles or timeline" ;;
-    tests-no2d) step tests-no2d 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-                 -k "not 2d and not blocks" ;;
-    tests-2d) step tests-2d 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-                 tests/test_gpu_engine.py tests/test_multiprocess_gpu.py -k "2d or blocks or native_cli" ;;
     mp) step mp 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_multiprocess_gpu.py ;;
     pcheck) step pcheck 300 python -u tools/pstream_check.py check ;;
     ptime) step ptime 300 python -u tools/pstream_check.py time ;;
     convtable) step convtable 600 python -u tools/conv_table.py ;;
-    pcols) step pcols 400 python -u tools/pstream_check.py cols ;;
-    pphases) step pphases 300 python -u tools/pstream_check.py phases ;;
-    sideweight) step sideweight 400 python -u tools/timeline.py 8192x4096:7:70 8192x4096:7:70:direct2d:side_weight=1.0 8192x4096:7:70:direct2d:side_weight=1.15 8192x4096:7:70:direct2d:side_weight=1.25 8192x4096:7:70:direct2d:side_weight=1.35 8192x4096:7:70:direct2d:side_weight=1.5 --json gpurun_out/sideweight.json ;;
     pmcpst) step pmcpst 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_VALU --kernel-trace --stats -d gpurun_out/pmcpst -o run -- python tools/prof_pstream.py 512 128 ;;
-    pksweep) step pksweep 300 python -u tools/pstream_check.py ksweep ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) step bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench1000) step bench1000 300 python bench.py --steps 1000 --warmup 200 ;;

@@ -61,6 +61,8 @@ def findings(ins: list) -> list:
         ws = 0
         for j in range(i + 1, min(len(ins), i + 8)):
             q = ins[j].replace(",", " ").split()
+            if q[0] == "s_endpgm":
+                break  # the wave ends here: what follows in the listing is another block
             if q[0] == "s_nop":
                 ws += int(q[1], 0) + 1
             else:

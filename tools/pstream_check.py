@@ -2,7 +2,8 @@
 launch-per-chunk kernel, alone and through the row-periodic direct IPC pipeline (the per-rank
 shape of 4096^2 strong scaling).
 
-Usage: python tools/pstream_check.py [check] [time]"""
+Usage: python tools/pstream_check.py [check] [time] [phases]
+(the round-3 depth and strip-width sweeps of profiles/pstream_r3.txt: git 6b5b463)"""
 import sys
 import time
 
@@ -81,31 +82,6 @@ if "time" in what:
                 del e
             print(f"time {nx}x{ny} K={K} steps={steps} direct={direct}: per-chunk {row[0]:.3f} us/step, "
                   f"persistent {row[1]:.3f} us/step ({row[0] / row[1]:.3f}x)", flush=True)
-
-if "ksweep" in what:
-    # halo depth = chunk depth K, direct row-periodic pipeline (the per-rank shape of strong scaling)
-    for nx in (512, 1024):
-        for K in (2, 3, 4, 5, 6, 7, 8):
-            row = []
-            for pers in (0, 1):
-                e = engine(nx, 4096, K, pers, direct=True)
-                row.append(timed(e, 840))
-                del e
-            print(f"ksweep {nx}x4096 K={K} direct: per-chunk {row[0]:.3f} us/step, persistent {row[1]:.3f} us/step",
-                  flush=True)
-
-
-if "cols" in what:
-    # strip width of the persistent kernel, direct row-periodic pipeline (per-rank strong-scaling tiles)
-    for nx in (512, 1024, 2048):
-        for K in (6, 7, 8):
-            row = []
-            for cols in (256, 128):
-                e = engine(nx, 4096, K, 1, direct=True, pstream_cols=cols)
-                row.append(timed(e, 840))
-                del e
-            print(f"cols {nx}x4096 K={K} direct persistent: 256-col {row[0]:.3f} us/step, 128-col {row[1]:.3f} us/step",
-                  flush=True)
 
 if "phases" in what:
     # where a chunk's time goes (per wave, per chunk, us): phase timers of the persistent kernel
