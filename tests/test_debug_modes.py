@@ -209,3 +209,21 @@ def test_host_sanitizers_engine_cpu_path(native, tmp_path):
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0 and r.stdout.startswith("ok 0"), r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_kernel_arguments_default_to_host_memory():
+    """Importing heat2d_amd selects host-memory kernel arguments for the HIP runtime unless the
+    user chose (docs/ARCHITECTURE.md, "Stale kernel arguments"); a fresh interpreter, so the
+    setting is seen before anything initialises the GPU."""
+    import subprocess
+    import sys
+
+    code = "import os, heat2d_amd; print(os.environ['HIP_FORCE_DEV_KERNARG'])"
+    env = {k: v for k, v in os.environ.items() if k != "HIP_FORCE_DEV_KERNARG"}
+    env["HEAT2D_NO_BUILD"] = "1"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
+    assert out.stdout.split()[-1] == "0"
+    env["HIP_FORCE_DEV_KERNARG"] = "1"  # the user's choice is kept
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
+    assert out.stdout.split()[-1] == "1"

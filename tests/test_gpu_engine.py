@@ -505,12 +505,13 @@ def _outside_nonzero(eng, t, b):
     return len(r), (_ranges(r - G), _ranges(c - PL)) if len(r) else None
 
 
-# The create-first engine order (a new engine built while the previous one is alive, the previous
-# one released right before the new run) is not run here: in the long GPU test process it made the
-# new engine's run compute wrong tiles, and once fault with an illegal memory access that poisoned
-# every later test of the process (docs/ARCHITECTURE.md, Known issues); in a fresh process it never
-# failed (tools/serial_repro.py create-first).
-_SERIAL_ORDERS = ["release-first"] + [o for o in os.environ.get("H2D_SERIAL_ORDERS", "").split(",") if o]
+# Engine orders: the previous engine released before the next is built (release-first), the
+# next built while the previous is alive and the previous released right before the run
+# (create-first: the plain `eng = Engine(...)` in a loop), and the previous kept alive through the
+# run (create-keep).  With the HIP runtime's kernel arguments in device memory, the create-* orders
+# computed wrong tiles in the long GPU test process and once faulted (stale kernel arguments:
+# docs/ARCHITECTURE.md); heat2d_amd keeps them in host memory by default, which this test checks.
+_SERIAL_ORDERS = ["release-first", "create-first", "create-keep"] + [o for o in os.environ.get("H2D_SERIAL_ORDERS", "").split(",") if o]
 
 
 @pytest.mark.parametrize("order", _SERIAL_ORDERS)
