@@ -23,7 +23,7 @@ step() {  # step NAME SECONDS CMD...: run, log, stop the script on failure
 
 for s in "$@"; do
   case "$s" in
-    tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     tests-nox) step tests-nox 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf ;;
     engine-file) step engine-file 600 python -u -m pytest tests/test_gpu_engine.py -q --timeout 300 --timeout-method thread -rf ;;
     serial) step serial 600 python -u -m pytest tests/test_gpu_engine.py -v --timeout 300 --timeout-method thread -rf -k serial_tiles_long ;;
@@ -41,6 +41,10 @@ for s in "$@"; do
                 --json gpurun_out/timeline.json ;;
     timeline2) step timeline2 300 python -u tools/timeline.py 512x4096:6:60 512x4096:6:60:direct 1024x4096:7:70 \
                  8192x4096:7:70 8192x4096:7:70:direct2d 4096x4096:7:70 --json gpurun_out/timeline2.json ;;
+    rehearse4) step rehearse4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+                 --master-port 29611 bench.py --gpus 4 --steps 42 --warmup 14 --persistent on ;;
+    rehearse8) step rehearse8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+                 --master-port 29612 bench.py --gpus 8 --steps 42 --warmup 14 --persistent on ;;
     proxy) step proxy 600 python -u tools/strong_proxy.py 4096 840 6,7,8 0 '' 1,2,4,8 ;;
     prof) step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
             python bench.py --steps 20 --warmup 5 --repeat 3 ;;
