@@ -45,6 +45,7 @@ for s in "$@"; do
                  --master-port 29611 bench.py --gpus 4 --steps 42 --warmup 14 --persistent on ;;
     rehearse8) step rehearse8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
                  --master-port 29612 bench.py --gpus 8 --steps 42 --warmup 14 --persistent on ;;
+    profconv) step profconv 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profconv -o run -- python tools/prof_conv.py 80 64 ;;
     proxy) step proxy 600 python -u tools/strong_proxy.py 4096 840 6,7,8 0 '' 1,2,4,8 ;;
     prof) step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
             python bench.py --steps 20 --warmup 5 --repeat 3 ;;
