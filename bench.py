@@ -50,12 +50,6 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# One solver per process, every timed result verified bit-exact in the job and every launch
-# integrity-checked: the bench keeps the HIP runtime's default of kernel arguments in device
-# memory (the library's default, host memory, costs +12 % per launch at 4096^2: 62.3 vs 55.5 us
-# per 7-step launch — docs/ARCHITECTURE.md, "Stale kernel arguments").  Export
-# HIP_FORCE_DEV_KERNARG=0 to time the library default.
-os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 # One hardware queue per engine stream (compute and comm must not share one: see
 # heat2d_amd/_native.py).  Read once at HIP initialisation, so it is set before torch starts.
 if os.environ.get("HEAT2D_KEEP_HW_QUEUES") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
@@ -425,7 +419,6 @@ def main() -> int:
                 "path": path,
                 "persistent_launches_per_rank": plaunches,
                 "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                "hip_force_dev_kernarg": os.environ.get("HIP_FORCE_DEV_KERNARG"),
             },
         }
         print(json.dumps(out), flush=True)

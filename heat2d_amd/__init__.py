@@ -8,26 +8,33 @@ xGMI between processes, a bit-exact CPU oracle.
 import os as _os
 import sys as _sys
 
-# Kernel arguments from host memory, not from the HIP runtime's device-memory kernarg pool: in a
-# process that creates many engines, launches read stale or torn arguments from that pool (the
-# integrity check's torn-argument bit fired; wrong tiles and an illegal access, gone with this
-# setting on the same box — docs/ARCHITECTURE.md, "Stale kernel arguments").  The HIP runtime
-# reads it when it initialises, so it is set before any GPU call; set it to 1 to opt out.
+# Kernel arguments from host memory, not from the HIP runtime's device-memory kernel-argument pool.
+# Under device-memory arguments the engine GPU tests fail in every configuration tried (round 4:
+# 5-6 of 612; round 5, with device-resident argument blocks, write-once metadata and a stream pool:
+# 4-29), and pass with host-memory arguments (docs/ARCHITECTURE.md, "Kernel arguments and metadata
+# memory").  The stencil kernels take their argument-block pointer and per-launch scalars as
+# preloaded SGPR arguments, so host-memory arguments cost nothing measurable (4096^2, K=7: 57.5 us
+# per launch against 57.8-58.1 with device-memory arguments).  The runtime reads the variable once,
+# at initialisation: set before any GPU call; a user's own setting is kept.
+KERNARG_HOST_MEMORY = _os.environ.get("HIP_FORCE_DEV_KERNARG") == "0"  # the effective state, once known
 if "HIP_FORCE_DEV_KERNARG" not in _os.environ:
     _torch = _sys.modules.get("torch")
     if _torch is not None and _torch.cuda.is_initialized():
         import warnings as _w
 
-        _w.warn("heat2d_amd imported after the GPU was initialised: HIP_FORCE_DEV_KERNARG=0 cannot take effect "
-                "(kernel arguments stay in device memory); import heat2d_amd first or export it", RuntimeWarning)
-    _os.environ["HIP_FORCE_DEV_KERNARG"] = "0"
+        # too late: the runtime already chose device-memory arguments; say so, change nothing
+        _w.warn("heat2d_amd imported after the GPU was initialised: kernel arguments stay in device memory "
+                "(import heat2d_amd first, or export HIP_FORCE_DEV_KERNARG=0)", RuntimeWarning)
+    else:
+        _os.environ["HIP_FORCE_DEV_KERNARG"] = "0"
+        KERNARG_HOST_MEMORY = True
 
 from ._native import native, gpu_available  # noqa: E402  (imports torch first: shared HIP runtime)
-from .config import Config, config_from_args, auto_grid
-from .models.heat2d import PRESETS, HeatModel, Preset
+from .config import Config, config_from_args, auto_grid  # noqa: E402
+from .models.heat2d import PRESETS, HeatModel, Preset  # noqa: E402
 
 __all__ = ["native", "gpu_available", "Config", "config_from_args", "auto_grid", "PRESETS", "HeatModel", "Preset",
-           "Solver"]
+           "Solver", "KERNARG_HOST_MEMORY"]
 __version__ = "0.1.0"
 
 

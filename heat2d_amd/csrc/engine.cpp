@@ -8,7 +8,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <thread>
 
@@ -21,6 +24,7 @@
   } while (0)
 
 namespace h2d {
+
 
 namespace {
 template <class T>
@@ -46,6 +50,53 @@ struct Roctx {
 Roctx& roctx() {
   static Roctx r;
   return r;
+}
+
+// Process-wide pool of non-blocking HIP streams, per (device, priority): an engine borrows its
+// two streams and hands them back, so a process creates streams — and the HIP runtime's
+// per-stream kernel-argument memory with them — once, not once per engine (round 5: a new
+// engine's first launches on freshly created streams read stale kernel arguments;
+// docs/ARCHITECTURE.md, "Kernel arguments").  HEAT2D_STREAM_POOL=0: create and destroy per engine.
+struct StreamPool {
+  std::mutex mu;
+  std::map<std::pair<int, int>, std::vector<hipStream_t>> free;  // never destroyed (process lifetime)
+};
+StreamPool& stream_pool() {
+  static StreamPool* p = new StreamPool();  // leaked: the runtime may be gone at static destruction
+  return *p;
+}
+bool stream_pool_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("HEAT2D_STREAM_POOL");
+    return e == nullptr || std::strcmp(e, "0") != 0;
+  }();
+  return on;
+}
+hipStream_t borrow_stream(int device, int prio) {
+  if (stream_pool_on()) {
+    StreamPool& P = stream_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto& v = P.free[{device, prio}];
+    if (!v.empty()) {
+      hipStream_t s = v.back();
+      v.pop_back();
+      return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  if (prio != 0) H2D_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));
+  else H2D_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return s;
+}
+void return_stream(int device, int prio, hipStream_t s) {  // (the caller has synchronised it)
+  if (s == nullptr) return;
+  if (!stream_pool_on()) {
+    hipStreamDestroy(s);
+    return;
+  }
+  StreamPool& P = stream_pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  P.free[{device, prio}].push_back(s);
 }
 }  // namespace
 
@@ -150,16 +201,15 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
       H2D_HIP_CHECK(hipExtStreamCreateWithCUMask(&compute_, (uint32_t)mc.size(), mc.data()));
       H2D_HIP_CHECK(hipExtStreamCreateWithCUMask(&comm_, (uint32_t)mx.size(), mx.data()));
     } else {
-      H2D_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+      compute_ = borrow_stream(o.device, 0);
       // Optionally a high-priority comm stream (its waves win dispatch ties against the
       // stencil's).  Separate hardware queues for compute and comm come from
       // GPU_MAX_HW_QUEUES >= 8 (set by the bench / CLI entry points), not from the priority.
       int least = 0, greatest = 0;
-      if (o.comm_priority > 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least) {
-        H2D_HIP_CHECK(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, greatest));
-      } else {
-        H2D_HIP_CHECK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
-      }
+      if (o.comm_priority > 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least)
+        comm_prio_ = greatest;
+      comm_ = borrow_stream(o.device, comm_prio_);
+      pooled_streams_ = true;
     }
     // Pipeline events only order work on this device (RCCL fences its own cross-device
     // traffic), so they can skip the system-scope fence.
@@ -359,10 +409,10 @@ Engine::~Engine() {
     for (int b = 0; b < 2; ++b) hipFree(t.buf[b]);
     if (t.keep) hipFree(t.keep);
   }
-  if (d_stop_) hipFree(d_stop_);
-  if (d_ticket_) hipFree(d_ticket_);
   if (h_conv_) hipHostFree(h_conv_);
   if (ev_check_) hipEventDestroy(ev_check_);
+  if (d_stop_) hipFree(d_stop_);
+  if (d_ticket_) hipFree(d_ticket_);
   for (auto& kv : pplans_) {
     hipFree(kv.second.d_units);
     hipFree(kv.second.d_prog);
@@ -379,18 +429,19 @@ Engine::~Engine() {
   hipFree(d_ipc_blocks_);
   hipFree(sig_counter_);
   hipFree(d_sig_timeout_);
-  if (h_timeout_) hipHostFree(h_timeout_);
   hipFree(halo_counter_);
   for (auto* m : {&local_descs_, &pack_descs_, &unpack_descs_})
     for (auto& kv : *m) hipFree(kv.second.d);
-  for (auto& t : tiles_) hipFree(t.partials);
+  for (auto& kv : ext_descs_) hipFree(kv.second.d);
   hipFree(d_lid_seen_);
   hipFree(d_resid_);
-  hipHostFree(h_resid_);
   hipFree(d_lds_steps_);
   hipFree(d_dummy_);
   hipFree(d_wait_acc_);
   if (d_phase_) hipFree(d_phase_);
+  if (h_timeout_) hipHostFree(h_timeout_);
+  for (auto& t : tiles_) hipFree(t.partials);
+  hipHostFree(h_resid_);
   if (d_stamps_) hipFree(d_stamps_);
   hipFree(d_send_);
   hipFree(d_recv_);
@@ -401,8 +452,13 @@ Engine::~Engine() {
   hipEventDestroy(ev_done_);
   for (auto& e : ev_prog_)
     if (e) hipEventDestroy(e);
-  hipStreamDestroy(compute_);
-  hipStreamDestroy(comm_);
+  if (pooled_streams_) {
+    return_stream(opt_.device, 0, compute_);
+    return_stream(opt_.device, comm_prio_, comm_);
+  } else {
+    hipStreamDestroy(compute_);
+    hipStreamDestroy(comm_);
+  }
 }
 
 void Engine::check_tile(int t) const {
@@ -608,7 +664,10 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   Tile& tl = tiles_[t];
   const TileGeom& g = tl.g;
   const UnitLists& L = units(t, K);
+  const hipStream_t ls = stream ? stream : compute_;
   StreamArgs a;
+  zero_args(a);
+  StreamDyn dy;
   if (src < 0) src = tl.cur;
   a.src = tl.buf[src];
   a.dst = tl.buf[1 - src];
@@ -644,8 +703,8 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     // the rollback copy: a lone tile recomputes it on convergence instead (no 4 B/cell write per check)
     if (residual && !recompute_rollback()) a.keep = tl.keep;
   }
-  // integrity: launch id at both ends of the arguments, the list's tag, the device error word
-  a.lid = a.lid_tail = (opt_.debug_kernel & 2) ? 0ull : ++lid_;
+  // integrity: launch id at both ends of the per-launch part, the list's tag, the device error word
+  dy.lid = (opt_.debug_kernel & 2) ? 0ull : ++lid_;
   a.dbg = opt_.debug_kernel;
   a.utag = L.tag[which];
   a.lid_seen = d_lid_seen_;
@@ -654,7 +713,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   if (transport_ == kTransportLocal && has_exchange_ && sig_mode_ == 0 && (stream == nullptr || stream == compute_)) {
     // serial local pipeline: the exchange copies in front of this launch on the compute stream
     a.copies_done = d_copies_done_;
-    a.copies_need = copies_need_;
+    dy.copies_need = copies_need_;
     a.waves_done = d_waves_done_;
   }
   if (which == 0) {
@@ -688,7 +747,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
       if (pn >= 0) {
         const IpcLayout& nl = ipc_lays_[pn];
         a.wait[0] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kN]);
-        a.need[0] = ipc_need_[kN];
+        dy.need[kN] = ipc_need_[kN];
         a.hsrc[0] = reinterpret_cast<const float*>(ipc_block_ + me.recv_n[p]);  // rows -G..-1
         a.push[0] = reinterpret_cast<float*>(ipc_blocks_[pn] + nl.recv_s[q]);   // N's rows xcell.. = my 0..
         a.sig[0] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pn] + nl.flag[kS]);
@@ -696,7 +755,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
       if (ps >= 0) {
         const IpcLayout& sl = ipc_lays_[ps];
         a.wait[1] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kS]);
-        a.need[1] = ipc_need_[kS];
+        dy.need[kS] = ipc_need_[kS];
         // ghost row i (xcell <= i < xcell+G) is receive row i - xcell
         a.hsrc[1] = reinterpret_cast<const float*>(ipc_block_ + me.recv_s[p] - (g.G + g.xcell) * rowb);
         // my row i (xcell-G <= i < xcell) is S's ghost row i - xcell, its receive row i - xcell + G
@@ -714,7 +773,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
         const int d = kW + i, pr = dec_.neighbor(tl.rank, d);
         if (pr < 0) continue;
         a.xwait[i] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[d]);
-        a.xneed[i] = ipc_need_[d];
+        dy.need[d] = ipc_need_[d];
         a.xsig[i] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pr] + ipc_lays_[pr].flag[kDirOpp[d]]);
         a.xpush[i] = side_push_base(d, pr, q);
         a.xpitch[i] = ipc_lays_[pr].pitch;
@@ -730,7 +789,7 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
       sig_target_ += (unsigned long long)L.n_boundary;
       if (dev_wait_) {
         a.wait[0] = a.wait[1] = halo_counter_;
-        a.need[0] = a.need[1] = halo_seq_;
+        dy.need[kN] = dy.need[kS] = halo_seq_;
       }
     }
   }
@@ -739,9 +798,12 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
     a.stamps = d_stamps_ + tl_recs_.size() * (size_t)kTimelineUnits * 4;
     tl_recs_.emplace_back(K, a.nunits);
   }
-  launch_stream(a, K, opt_.precision, residual, stream ? stream : compute_);
+  const StreamArgs* blk = args_.get(a, ls);  // the plan-constant part: device-resident, uploaded once
+  dy.nunits = a.nunits;
+  dy.btag = a.head.btag;
+  launch_stream(blk, a, dy, K, opt_.precision, residual, ls);
   if (a.waves_done != nullptr) waves_need_ += (unsigned long long)a.nunits;
-  progress_tick(stream ? stream : compute_);
+  progress_tick(ls);
   if (residual && whole && !lone) reduce_tile_residual(t, K);
   if (residual && whole && lone) {
     last_parts_ = tl.partials;
@@ -822,6 +884,15 @@ Engine::DescList Engine::upload_descs(std::vector<CopyDesc>& v) {
     std::copy(v.begin(), v.end(), L.d);
   }
   return L;
+}
+
+const Engine::DescList& Engine::ext_descs(std::vector<CopyDesc>& v) {
+  // the caller-driven pack / unpack lists (external transports): one upload per distinct list
+  // (the descriptors name the caller's buffers), from the metadata arena
+  std::string key(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(CopyDesc));
+  auto it = ext_descs_.find(key);
+  if (it != ext_descs_.end()) return it->second;
+  return ext_descs_.emplace(std::move(key), upload_descs(v)).first->second;
 }
 
 const Engine::DescList& Engine::local_descs(int K) {
@@ -1230,6 +1301,8 @@ void Engine::run_tiled(RunStats& st, int64_t target) {
       k = chunk_len(steps_done_, target, tile_k_, &check);
     }
     TileArgs a;
+    zero_args(a);
+    TileDyn dy;
     a.src = T.buf[T.cur] + T.g.idx(0, 0);
     a.dst = T.buf[1 - T.cur] + T.g.idx(0, 0);
     a.pitch = T.g.pitch;
@@ -1251,6 +1324,8 @@ void Engine::run_tiled(RunStats& st, int64_t target) {
       a.pend = T.partials + (size_t)(pset ^ 1) * (size_t)(T.pcap / 2);
       a.pend_n = pend_n;
       a.pend_dec = pend_dec;
+      a.pend_dec.seq = 0;  // (per launch: TileDyn::pend_seq)
+      dy.pend_seq = pend_dec.seq;
       pend = false;
     }
     if (fused_) {
@@ -1266,12 +1341,17 @@ void Engine::run_tiled(RunStats& st, int64_t target) {
           pset ^= 1;
         } else {
           a.dec = decide_args(0, true);  // the last block sums the partials and decides
+          dy.seq = a.dec.seq;
+          a.dec.seq = 0;  // (per launch: TileDyn::seq)
         }
         decided_in_launch_ = true;
       }
     }
     trace_begin("step", compute_);
-    launch_tile(a, opt_.precision, check, compute_);
+    prepare_tile(a);
+    const TileArgs* blk = args_.get(a, compute_);  // the plan-constant part: device-resident
+    dy.btag = a.head.btag;
+    launch_tile(blk, a, dy, opt_.precision, check, compute_);
     trace_end("step", compute_);
     if (check && !fused_) launch_reduce_sum(a.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
     T.cur = 1 - T.cur;
@@ -1568,14 +1648,18 @@ void Engine::launch_pstream_chunks(int K, int J) {
   Tile& T = tiles_[0];
   const TileGeom& g = T.g;
   PStreamArgs a;
+  zero_args(a);
+  a.rel = 2;
+  a.acq = 1;
+  PStreamDyn dy;
   a.units = P.d_units;
   a.nunits = P.n;
-  a.nchunks = J;
-  a.cbase = P.cdone;
+  dy.nunits = P.n;
+  dy.nchunks = J;
+  dy.cbase = P.cdone;
   a.buf[0] = T.buf[0];
   a.buf[1] = T.buf[1];
-  a.cur0 = T.cur;
-  a.src0 = T.buf[T.cur];
+  dy.cur0 = T.cur;
   a.prog = P.d_prog;
   a.pitch = g.pitch;
   a.G = g.G;
@@ -1605,7 +1689,7 @@ void Engine::launch_pstream_chunks(int K, int J) {
     if (pn >= 0) {
       const IpcLayout& nl = ipc_lays_[pn];
       a.wait[0] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kN]);
-      a.need0[0] = ipc_need_[kN];
+      dy.need0[0] = ipc_need_[kN];
       a.need_inc[0] = (unsigned long long)pst_counts_[pn].at((size_t)K * 2 + 1);  // N's south pushes
       a.sig[0] = reinterpret_cast<unsigned long long*>(ipc_blocks_[pn] + nl.flag[kS]);
       for (int p = 0; p < 2; ++p) {
@@ -1616,7 +1700,7 @@ void Engine::launch_pstream_chunks(int K, int J) {
     if (ps >= 0) {
       const IpcLayout& sl = ipc_lays_[ps];
       a.wait[1] = reinterpret_cast<const unsigned long long*>(ipc_block_ + me.flag[kS]);
-      a.need0[1] = ipc_need_[kS];
+      dy.need0[1] = ipc_need_[kS];
       a.need_inc[1] = (unsigned long long)pst_counts_[ps].at((size_t)K * 2 + 0);  // S's north pushes
       a.sig[1] = reinterpret_cast<unsigned long long*>(ipc_blocks_[ps] + sl.flag[kN]);
       for (int p = 0; p < 2; ++p) {
@@ -1624,19 +1708,21 @@ void Engine::launch_pstream_chunks(int K, int J) {
         a.push[1][p] = reinterpret_cast<float*>(ipc_blocks_[ps] + sl.recv_n[p] - (g.xcell - g.G) * rowb);
       }
     }
-    a.ipar0 = (int)(ipc_chunk_ & 1);
+    dy.ipar0 = (int)(ipc_chunk_ & 1);
     a.sig_rows = G_;
     for (int d = 0; d < 2; ++d) {  // chunk order of my halo units' signals (PStreamArgs::lsig)
       // (debug_kernel bit 4: without the chunk order — diagnostics only, races between processes)
       a.lsig[d] = (opt_.debug_kernel & 4) ? nullptr : reinterpret_cast<unsigned long long*>(ipc_block_ + me.lsig[d]);
-      a.lbase[d] = ipc_lsig_[d];
+      dy.lbase[d] = ipc_lsig_[d];
       a.lper[d] = P.pushes[d];
       ipc_lsig_[d] += (unsigned long long)J * (unsigned long long)P.pushes[d];
     }
     a.rel = opt_.direct_release < 0 ? 2 : opt_.direct_release;
     a.acq = opt_.direct_acquire < 0 ? 1 : opt_.direct_acquire;
   }
-  launch_pstream(a, K, opt_.precision, P.cpl, compute_);
+  const PStreamArgs* blk = args_.get(a, compute_);  // the plan-constant part: device-resident
+  dy.btag = a.head.btag;
+  launch_pstream(blk, dy, K, opt_.precision, P.cpl, opt_.pstream_pingpong > 0, compute_);
   P.cdone += (unsigned)J;
   ++pstream_launches_;
   progress_tick(compute_);
@@ -1818,13 +1904,9 @@ void Engine::pack(int t, int k, uintptr_t sendbuf) {
   plan_pack_descs(p, T.g, T.buf[T.cur], reinterpret_cast<float*>(sendbuf), v);
   if (on_gpu()) {
     if (v.empty()) return;
-    int64_t me = 0;
-    for (auto& c : v) me = std::max(me, c.rows * c.cols);
-    CopyDesc* d = dmalloc<CopyDesc>(v.size());
-    H2D_HIP_CHECK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(CopyDesc), hipMemcpyHostToDevice, compute_));
-    launch_copy_rects(d, (int)v.size(), me, compute_);
+    const DescList& D = ext_descs(v);
+    launch_copy_rects(D.d, D.n, D.maxe, compute_, D.tag, nullptr, d_sig_timeout_, h_timeout_dev_);
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
-    hipFree(d);
   } else {
     cpu_copy_rects(v);
   }
@@ -1838,13 +1920,9 @@ void Engine::unpack(int t, int k, uintptr_t recvbuf) {
   plan_unpack_descs(p, T.g, T.buf[T.cur], reinterpret_cast<const float*>(recvbuf), v);
   if (on_gpu()) {
     if (v.empty()) return;
-    int64_t me = 0;
-    for (auto& c : v) me = std::max(me, c.rows * c.cols);
-    CopyDesc* d = dmalloc<CopyDesc>(v.size());
-    H2D_HIP_CHECK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(CopyDesc), hipMemcpyHostToDevice, compute_));
-    launch_copy_rects(d, (int)v.size(), me, compute_);
+    const DescList& D = ext_descs(v);
+    launch_copy_rects(D.d, D.n, D.maxe, compute_, D.tag, nullptr, d_sig_timeout_, h_timeout_dev_);
     H2D_HIP_CHECK(hipStreamSynchronize(compute_));
-    hipFree(d);
   } else {
     cpu_copy_rects(v);
   }

@@ -99,6 +99,9 @@ struct EngineOptions {
   // Waves of one persistent launch at most (0: one per SIMD of the device).  Ranks that share a
   // GPU (a one-GPU rehearsal of an N-GPU run) split it, so every rank's waves are resident at once.
   int pstream_waves = 0;
+  // Steady loop of the persistent kernel: 1 loads the next rows a whole iteration ahead
+  // (ping-pong register sets), 0 / -1 row by row as they are consumed (the measured default).
+  int pstream_pingpong = -1;
   // 2-D direct pipeline: cost weight per row of the units that push to a W / E neighbour
   double side_weight = 1.35;
   // Diagnostics: per-phase timers of the persistent kernel (PStreamArgs::phase)
@@ -323,9 +326,14 @@ class Engine {
 
   // device state
   hipStream_t compute_ = nullptr, comm_ = nullptr;
+  bool pooled_streams_ = false;  // borrowed from the process-wide stream pool (engine.cpp)
+  int comm_prio_ = 0;
   hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr, ev_t0_ = nullptr, ev_t1_ = nullptr, ev_done_ = nullptr;
   void end_of_run_wait(RunStats& st, std::chrono::steady_clock::time_point w0);
   std::map<std::pair<int, int>, UnitLists> units_;
+  // device-resident kernel-argument blocks of this engine's launches (kernels.h); destroyed after
+  // the destructor's device synchronisation
+  ArgBlocks args_;
   // an uploaded copy-descriptor list: n descriptors, the largest rectangle, its integrity tag
   struct DescList {
     CopyDesc* d = nullptr;
@@ -335,6 +343,8 @@ class Engine {
   };
   DescList upload_descs(std::vector<CopyDesc>& v);  // tags and uploads (GPU) or keeps (CPU) a list
   const DescList& local_descs(int K);
+  const DescList& ext_descs(std::vector<CopyDesc>& v);  // pack / unpack lists, by content
+  std::map<std::string, DescList> ext_descs_;
   void local_copy(const DescList& D, hipStream_t s);  // one local exchange (tagged, counted on compute_)
   std::map<std::pair<int, int>, DescList> local_descs_;  // (K, parity)
   std::map<std::pair<int, int>, DescList> pack_descs_;   // (K, parity) for rccl

@@ -259,8 +259,8 @@ RunStats run_external(Engine& e, Bootstrap& boot, int64_t steps, double sensitiv
 }  // namespace
 
 int main(int argc, char** argv) {
-  // kernel arguments from host memory (docs/ARCHITECTURE.md, "Stale kernel arguments"); before
-  // any HIP call, and only if the user did not choose
+  // kernel arguments from host memory (docs/ARCHITECTURE.md, "Kernel arguments and metadata
+  // memory"); before any HIP call, and only if the user did not choose
   setenv("HIP_FORCE_DEV_KERNARG", "0", 0);
   std::map<std::string, std::string> a;
   for (int i = 1; i < argc; ++i) {

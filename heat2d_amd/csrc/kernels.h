@@ -3,10 +3,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "h2d_common.h"
@@ -94,7 +98,8 @@ struct ConvHost {
 // Convergence decision of check `seq` made on the device by whoever holds the total: the last
 // wave of a residual launch (fused epilogue), or a reduction kernel.  ticket != nullptr: the
 // launch's residual partials are summed and decided in-kernel by the wave whose ticket add
-// comes last (it resets the ticket for the next check).
+// comes last (it resets the ticket for the next check).  Inside a device-resident argument block
+// `seq` is not used: the check number is a per-launch value (StreamDyn::seq, TileDyn::seq).
 struct DecideArgs {
   unsigned int* ticket = nullptr;
   double* total = nullptr;
@@ -107,19 +112,49 @@ struct DecideArgs {
 // Integrity bits of the engine's device error word (StreamArgs::timed_out, shared with the
 // bounded-wait timeouts 1/2/4/8): a launch that sees inconsistent inputs reports instead of
 // computing on them, and the host names the cause (Engine::poll_abort).
-constexpr unsigned kIntegArgs = 16u;     // kernel arguments torn: head and tail launch ids differ
+constexpr unsigned kIntegArgs = 16u;     // kernel arguments: torn per-launch part, or a block the launch does not name
 constexpr unsigned kIntegUnits = 32u;    // a unit's tag is not the tag of the list the launch names
 constexpr unsigned kIntegReplay = 64u;   // a launch ran with the arguments of an earlier launch
 constexpr unsigned kIntegDescs = 128u;   // a copy descriptor's tag is not the list's tag
 constexpr unsigned kIntegOrder = 256u;   // a stencil launch started before its exchange copy finished
 constexpr unsigned kIntegOrder2 = 512u;  // an exchange copy started before the stencil launches before it finished
 
-// Arguments of the temporally-blocked streaming stencil.
-struct StreamArgs {
-  // launch id (engine launches: > 0, increasing in stream order; 0: no integrity checks).  The
-  // same id is the struct's LAST member too, so the two ends of the kernel-argument block are
-  // compared by every wave.
+// ---- kernel arguments: device-resident blocks + a small per-launch part ---------------------
+// The stencil kernels take (1) a pointer to an immutable, device-resident argument block with
+// everything a plan fixes — buffers, unit lists, geometry, halo wiring — and (2) a small by-value
+// struct with what changes per launch (launch id, halo counts, chunk numbers, check number).
+// Blocks are uploaded once per distinct content (ArgBlocks) and never rewritten while any launch
+// can read them, so a launch reads only ~100 bytes of kernel arguments, once per wave — which
+// makes the library's host-memory kernel arguments free (round 4's ~750-byte by-value structs
+// cost +12 % per launch there: docs/ARCHITECTURE.md, "Kernel arguments").
+// Every block starts with this header: ArgBlocks stamps a process-wide tag into it, the launch
+// passes the same tag by value, and the kernel compares the two (kIntegArgs).
+struct ArgHead {
+  unsigned btag = 0;
+  unsigned bytes = 0;
+};
+
+// Per-launch part of a streaming launch.
+struct StreamDyn {
+  // launch id (engine launches: > 0, increasing in stream order; 0: no integrity checks)
   unsigned long long lid = 0;
+  // halo counts this launch's halo units wait for, per direction (Dir: N, S, W, E, NW, NE, SW, SE)
+  unsigned long long need[kNumDirs] = {};
+  unsigned long long copies_need = 0;  // serial pipeline: exchange copy blocks completed before this launch
+  unsigned long long seq = 0;          // check number of a deciding residual launch (DecideArgs::seq)
+  int nunits = 0;                      // == the block's nunits (the launcher's grid size)
+  unsigned btag = 0;                   // the block's ArgHead::btag
+};
+// The kernel receives the per-launch scalars as separate scalar kernel arguments, read once at the
+// wave's start with the block pointer (kept in SGPRs, never reloaded); the halo counts come by
+// value behind them and only halo units read them.
+struct StreamNeed {
+  unsigned long long v[kNumDirs];
+};
+
+// Arguments of the temporally-blocked streaming stencil (the device-resident block).
+struct StreamArgs {
+  ArgHead head;
   const float* src;
   float* dst;
   const Unit* units;
@@ -139,7 +174,7 @@ struct StreamArgs {
   int prot = 0;
   // Halo units [0, nsignal) of the signalled / direct pipelines.  Direction d of a unit: 0 = a
   // top unit (its ghost rows are the north halo), 1 = a bottom unit (kUnitReverse, south halo).
-  //   wait[d]/need[d]: before reading ghost rows, poll *wait[d] until it reaches need[d]
+  //   wait[d]:         before reading ghost rows, poll *wait[d] until it reaches StreamDyn::need[d]
   //                    (bounded: after halo_polls polls give up and report a timeout);
   //   hsrc[d]:         read the ghost rows from here instead of src (storage-equivalent base:
   //                    ghost row i lives at hsrc[d] + (G + i) * pitch + PL);
@@ -152,7 +187,7 @@ struct StreamArgs {
   int nsignal = 0;
   int sig_rows = 0;
   // 2-D direct pipeline, side links (index = Dir - 2: W, E, NW, NE, SW, SE):
-  //   xwait[i]/xneed[i]: my flag for pushes from that neighbour and the count this chunk needs;
+  //   xwait[i]:          my flag for pushes from that neighbour (this chunk needs StreamDyn::need[2 + i]);
   //   xsig[i]:           that neighbour's flag for my pushes;
   //   gsrc[0/1]:         my W / E ghost-column group of this chunk's parity — ghost column j of
   //                      row i lives at gsrc[0] + (G + i) * pitch + kGhostGroup + j (j < 0) and
@@ -160,14 +195,12 @@ struct StreamArgs {
   //   xpush[i]/xpitch[i]: my cell (i, j) that belongs to that neighbour's halo is stored at
   //                      xpush[i] + i * xpitch[i] + j (the host folds every offset into xpush).
   const unsigned long long* xwait[kSideLinks] = {};
-  unsigned long long xneed[kSideLinks] = {};
   unsigned long long* xsig[kSideLinks] = {};
   const float* gsrc[2] = {nullptr, nullptr};
   float* xpush[kSideLinks] = {};
   int64_t xpitch[kSideLinks] = {};
   unsigned long long* sig[2] = {nullptr, nullptr};
   const unsigned long long* wait[2] = {nullptr, nullptr};
-  unsigned long long need[2] = {0, 0};
   const float* hsrc[2] = {nullptr, nullptr};
   float* push[2] = {nullptr, nullptr};
   // Device-side convergence (fused check): a launch whose *stop is non-zero does nothing (its
@@ -193,16 +226,15 @@ struct StreamArgs {
   // end, hardware id (XCC_ID << 16 | HW_ID[15:0])}.
   unsigned long long* wait_acc = nullptr;
   unsigned long long* stamps = nullptr;
-  // integrity (lid > 0): the tag every unit of `units` carries; the engine's highest launch id
-  // seen (wave 0 raises it at its end — an old value >= lid is a replayed launch); serial
-  // pipeline: the exchange copy blocks completed so far must equal copies_need at wave 0's start
+  // integrity (StreamDyn::lid > 0): the tag every unit of `units` carries; the engine's highest
+  // launch id seen (wave 0 raises it — an old value >= lid is a replayed launch); serial
+  // pipeline: the exchange copy blocks completed so far must equal StreamDyn::copies_need at
+  // wave 0's start
   int utag = 0;
   int dbg = 0;  // diagnostics (EngineOptions::debug_kernel): 1 every unit runs the halo bodies
   unsigned long long* lid_seen = nullptr;
   const unsigned long long* copies_done = nullptr;
-  unsigned long long copies_need = 0;
   unsigned long long* waves_done = nullptr;  // serial pipeline: every wave adds 1 at its end (its stores drained)
-  unsigned long long lid_tail = 0;
 };
 
 // ---- persistent pipelined streaming stencil (pstream_kernel.hpp) ---------------------------
@@ -221,14 +253,22 @@ struct PUnit {
   // output index of my stream row r is qa + qs * r (qs = +-1); its rows per chunk hv
   int nb[kPSlots], rlo[kPSlots], rhi[kPSlots], qa[kPSlots], qs[kPSlots], hv[kPSlots];
 };
+// Per-launch part of a persistent launch.
+struct PStreamDyn {
+  int nunits = 0;          // == the block's nunits (the launcher's grid size)
+  int nchunks = 0;         // J (>= 1)
+  unsigned cbase = 0;      // chunks this plan completed in earlier launches (progress base)
+  int cur0 = 0;            // chunk j reads buf[(cur0 + j) & 1]
+  int ipar0 = 0;           // receive-buffer parity of chunk 0 (direct pipeline)
+  unsigned btag = 0;       // the block's ArgHead::btag
+  unsigned long long need0[2] = {0, 0};  // halo flag counts chunk 0 waits for (N / S)
+  unsigned long long lbase[2] = {0, 0};  // my halo units' signals before the launch (N / S, chunk order)
+};
 struct PStreamArgs {
+  ArgHead head;
   const PUnit* units;
   int nunits;
-  int nchunks;          // J (>= 1)
-  unsigned cbase;       // chunks this plan completed in earlier launches (progress base)
-  const float* src0;    // buffer read by chunk 0 (chunk j reads buf[(cur0 + j) & 1])
   float* buf[2];
-  int cur0;
   unsigned* prog;       // progress words, 32 apart (one 128-B line each)
   int64_t pitch, G, PL;
   int64_t xcell, ycell;
@@ -239,21 +279,21 @@ struct PStreamArgs {
   int dbg = 0;  // diagnostics (EngineOptions::debug_kernel): 1 every unit runs the halo-unit bodies
   float* dummy;
   // direct (IPC) halo units, per direction (0 north / top band, 1 south / bottom band, reverse)
-  // and receive-buffer parity: chunk j reads parity (ipar0 + j) & 1 and pushes to the other
+  // and receive-buffer parity: chunk j reads parity (PStreamDyn::ipar0 + j) & 1 and pushes to
+  // the other; chunk j waits for PStreamDyn::need0[d] + j * need_inc[d] on wait[d]
   const unsigned long long* wait[2] = {nullptr, nullptr};
-  unsigned long long need0[2] = {0, 0}, need_inc[2] = {0, 0};
+  unsigned long long need_inc[2] = {0, 0};
   // chunk order of the signals: a halo unit signals chunk j of the launch only once all of this
-  // rank's halo units of its direction have signalled chunk j-1 (*lsig[d] counts them, lbase[d]
-  // before the launch, lper[d] per chunk).  The neighbour's wait counts pushes summed over ALL
-  // strips, so without it a strip running a chunk ahead could stand in for a slow strip's missing
-  // push and the neighbour would read that strip's ghost rows before they landed.
+  // rank's halo units of its direction have signalled chunk j-1 (*lsig[d] counts them,
+  // PStreamDyn::lbase[d] before the launch, lper[d] per chunk).  The neighbour's wait counts
+  // pushes summed over ALL strips, so without it a strip running a chunk ahead could stand in
+  // for a slow strip's missing push and the neighbour would read that strip's ghost rows before
+  // they landed.
   unsigned long long* lsig[2] = {nullptr, nullptr};
-  unsigned long long lbase[2] = {0, 0};
   int lper[2] = {0, 0};
   const float* hsrc[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   float* push[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   unsigned long long* sig[2] = {nullptr, nullptr};
-  int ipar0 = 0;
   int sig_rows = 0;
   int rel = 2, acq = 1;
   long long halo_polls = 0;
@@ -270,8 +310,11 @@ struct PStreamArgs {
 constexpr int kPhases = 7;
 // Largest K with a compiled persistent kernel (K <= 8, write-through stores).
 constexpr int kMaxPK = 8;
-// cpl: columns per lane of the plan (4 or 2), a template parameter of the kernel.
-void launch_pstream(const PStreamArgs& a, int K, int precision, int cpl, hipStream_t s);
+// cpl: columns per lane of the plan (4 or 2), a template parameter of the kernel.  `blk`: the
+// device-resident block (ArgBlocks).
+// pingpong: the steady loop variant that loads the next rows a whole iteration ahead
+void launch_pstream(const PStreamArgs* blk, const PStreamDyn& d, int K, int precision, int cpl, bool pingpong,
+                    hipStream_t s);
 // Resident 256-thread blocks per CU of the persistent kernel (every block must be resident).
 int pstream_blocks_per_cu(int K, int precision, int cpl);
 void warm_pstream_kernels(int precision, int kmax, hipStream_t s);
@@ -285,7 +328,10 @@ std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x
 constexpr int kMaxK = 16;
 bool stream_k_supported(int K);
 
-void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hipStream_t s);
+// `blk`: the device-resident block (ArgBlocks), whose host copy `host` the launcher checks
+// (geometry against K, store flavour); d.nunits == 0 launches nothing.
+void launch_stream(const StreamArgs* blk, const StreamArgs& host, const StreamDyn& d, int K, int precision,
+                   bool residual, hipStream_t s);
 // No-op launches of every compiled streaming kernel with K <= kmax (both residual variants of
 // `precision`), so that no code object is first loaded inside a timed run (one TU per K).
 void warm_stream_kernels(int precision, int kmax, hipStream_t s);
@@ -337,11 +383,69 @@ namespace h2d {
 // per-variant launch / occupancy of the streaming kernel (stream_kernel.hpp; instantiated in
 // generated TUs, one per (K, precision, residual))
 template <int K, bool F32, bool RESID>
-void launch_stream_kv(const StreamArgs& a, hipStream_t s);
+void launch_stream_kv(const StreamArgs* blk, const StreamDyn& d, bool wt, hipStream_t s);  // (unpacks d)
 template <int K, bool F32, bool RESID>
 int stream_blocks_per_cu_v();
 template <int K, bool F32, int CPL>
-void launch_pstream_kv(const PStreamArgs& a, hipStream_t s);
+void launch_pstream_kv(const PStreamArgs* blk, const PStreamDyn& d, bool pingpong, hipStream_t s);
 template <int K, bool F32, int CPL>
 int pstream_blocks_per_cu_v();
+
+// Immutable device-resident kernel-argument blocks, deduplicated by content.
+//
+// get(a, s) returns the device copy of the bytes of `a` (ArgHead excluded from the comparison):
+// the first time, the bytes go to a pinned host slab and a one-wave copy kernel on stream `s`
+// writes them into device memory — ordered before every later launch on `s`, no host wait, and
+// written through the L2 that the kernels' scalar loads read (a DMA engine writes around it).
+// A block is never rewritten and lives until the owner is destroyed (after a device sync), so
+// no launch can see a block change under it.  A block first used on another stream waits for
+// its upload once (host sync of the uploading stream).
+class ArgBlocks {
+ public:
+  ArgBlocks() = default;
+  ~ArgBlocks();
+  ArgBlocks(const ArgBlocks&) = delete;
+  ArgBlocks& operator=(const ArgBlocks&) = delete;
+  template <class T>
+  const T* get(T& a, hipStream_t s) {
+    static_assert(offsetof(T, head) == 0, "argument blocks start with an ArgHead");
+    return static_cast<const T*>(get_raw(&a, sizeof(T), &a.head, s));
+  }
+  size_t blocks() const { return n_blocks_; }
+  size_t uploads() const { return n_uploads_; }
+  size_t bytes() const { return n_bytes_; }
+  // Free every block (the caller has synchronised the device).  Cap for long-lived caches
+  // (bindings' op API): callers clear when blocks() exceeds their bound.
+  void clear();
+ private:
+  // fills *head (tag, size) and returns the device block
+  const void* get_raw(const void* p, size_t n, ArgHead* head, hipStream_t s);
+  struct Slab {
+    char* dev = nullptr;
+    char* host = nullptr;  // pinned, the kernel's copy source
+    size_t cap = 0, used = 0;
+  };
+  struct Entry {
+    const void* dev;
+    unsigned tag;
+    hipStream_t stream;  // uploaded on
+    bool ready;          // the upload is known complete (usable on any stream)
+  };
+  std::vector<Slab> slabs_;
+  std::unordered_map<std::string, Entry> index_;  // by content (the bytes after the ArgHead)
+  size_t n_blocks_ = 0, n_uploads_ = 0, n_bytes_ = 0;
+};
+// Process-wide block tags (never 0).
+unsigned next_arg_tag();
+
+// Argument structs are filled from all-zero bytes, padding included (ArgBlocks deduplicates
+// blocks by their bytes; every member's default is zero except where the caller sets one).
+template <class T>
+inline void zero_args(T& a) {
+  std::memset(static_cast<void*>(&a), 0, sizeof(T));
+}
+// A device block of kZeroArgBytes zero bytes (per device, allocated once): the argument block of
+// no-op launches (warm_*_kernels: a zero unit / tile count).
+constexpr size_t kZeroArgBytes = 4096;
+const void* zero_arg_block();
 }  // namespace h2d

@@ -5,6 +5,10 @@
 #include "stream_kernel.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace h2d {
@@ -296,24 +300,24 @@ __global__ __launch_bounds__(1024) void lds_solver_kernel(const float* __restric
 #define H2D_K_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(12) X(16)
 // The variants live in generated translation units (heat2d_amd/_build.py: K_LIST there must
 // match this list).
-#define H2D_EXTERN(K)                                                                          \
-  extern template void launch_stream_kv<K, false, false>(const StreamArgs&, hipStream_t);      \
-  extern template void launch_stream_kv<K, false, true>(const StreamArgs&, hipStream_t);       \
-  extern template void launch_stream_kv<K, true, false>(const StreamArgs&, hipStream_t);       \
-  extern template void launch_stream_kv<K, true, true>(const StreamArgs&, hipStream_t);        \
+#define H2D_EXTERN(K)                                                                                          \
+  extern template void launch_stream_kv<K, false, false>(const StreamArgs*, const StreamDyn&, bool, hipStream_t); \
+  extern template void launch_stream_kv<K, false, true>(const StreamArgs*, const StreamDyn&, bool, hipStream_t);  \
+  extern template void launch_stream_kv<K, true, false>(const StreamArgs*, const StreamDyn&, bool, hipStream_t);  \
+  extern template void launch_stream_kv<K, true, true>(const StreamArgs*, const StreamDyn&, bool, hipStream_t);   \
   extern template int stream_blocks_per_cu_v<K, false, false>();                                \
   extern template int stream_blocks_per_cu_v<K, true, false>();
 H2D_K_LIST(H2D_EXTERN)
 #undef H2D_EXTERN
 
 template <int K>
-void launch_stream_k(const StreamArgs& a, bool f32, bool resid, hipStream_t s) {
+void launch_stream_k(const StreamArgs* blk, const StreamDyn& d, bool wt, bool f32, bool resid, hipStream_t s) {
   if (f32) {
-    if (resid) launch_stream_kv<K, true, true>(a, s);
-    else launch_stream_kv<K, true, false>(a, s);
+    if (resid) launch_stream_kv<K, true, true>(blk, d, wt, s);
+    else launch_stream_kv<K, true, false>(blk, d, wt, s);
   } else {
-    if (resid) launch_stream_kv<K, false, true>(a, s);
-    else launch_stream_kv<K, false, false>(a, s);
+    if (resid) launch_stream_kv<K, false, true>(blk, d, wt, s);
+    else launch_stream_kv<K, false, false>(blk, d, wt, s);
   }
 }
 
@@ -524,12 +528,15 @@ bool stream_k_supported(int K) {
   }
 }
 
-void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hipStream_t s) {
+void launch_stream(const StreamArgs* blk, const StreamArgs& a, const StreamDyn& d, int K, int precision,
+                   bool residual, hipStream_t s) {
   if (a.nunits <= 0) return;
   if (lead_cols(K) != a.R || kWaveCols - 2 * a.R != a.wout) throw std::invalid_argument("launch_stream: R/wout mismatch");
+  if (blk == nullptr || d.nunits != a.nunits || d.btag != a.head.btag)
+    throw std::invalid_argument("launch_stream: the launch does not name its argument block");
   const bool f32 = precision == kFp32;
   switch (K) {
-#define H2D_CASE(KK) case KK: launch_stream_k<KK>(a, f32, residual, s); break;
+#define H2D_CASE(KK) case KK: launch_stream_k<KK>(blk, d, a.wt != 0, f32, residual, s); break;
     H2D_K_LIST(H2D_CASE)
 #undef H2D_CASE
     default: throw std::invalid_argument("no streaming kernel compiled for K=" + std::to_string(K));
@@ -539,11 +546,11 @@ void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hip
 
 // ---- persistent pipelined variant (pstream_kernel.hpp, generated TUs pstream_k<K>_f<F>.hip) ----
 #define H2D_PK_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
-#define H2D_PEXTERN(K)                                                                 \
-  extern template void launch_pstream_kv<K, false, 4>(const PStreamArgs&, hipStream_t); \
-  extern template void launch_pstream_kv<K, true, 4>(const PStreamArgs&, hipStream_t);  \
-  extern template void launch_pstream_kv<K, false, 2>(const PStreamArgs&, hipStream_t); \
-  extern template void launch_pstream_kv<K, true, 2>(const PStreamArgs&, hipStream_t);  \
+#define H2D_PEXTERN(K)                                                                                      \
+  extern template void launch_pstream_kv<K, false, 4>(const PStreamArgs*, const PStreamDyn&, bool, hipStream_t); \
+  extern template void launch_pstream_kv<K, true, 4>(const PStreamArgs*, const PStreamDyn&, bool, hipStream_t);  \
+  extern template void launch_pstream_kv<K, false, 2>(const PStreamArgs*, const PStreamDyn&, bool, hipStream_t); \
+  extern template void launch_pstream_kv<K, true, 2>(const PStreamArgs*, const PStreamDyn&, bool, hipStream_t);  \
   extern template int pstream_blocks_per_cu_v<K, false, 4>();                           \
   extern template int pstream_blocks_per_cu_v<K, true, 4>();                            \
   extern template int pstream_blocks_per_cu_v<K, false, 2>();                           \
@@ -551,14 +558,16 @@ void launch_stream(const StreamArgs& a, int K, int precision, bool residual, hip
 H2D_PK_LIST(H2D_PEXTERN)
 #undef H2D_PEXTERN
 
-void launch_pstream(const PStreamArgs& a, int K, int precision, int cpl, hipStream_t s) {
+void launch_pstream(const PStreamArgs* blk, const PStreamDyn& d, int K, int precision, int cpl, bool pp,
+                    hipStream_t s) {
   const bool f32 = precision == kFp32;
   if (cpl != 2 && cpl != 4) throw std::invalid_argument("persistent stencil: 2 or 4 columns per lane");
+  if (blk == nullptr) throw std::invalid_argument("persistent stencil: no argument block");
   switch (K) {
-#define H2D_CASE(KK)                                                                             \
-  case KK:                                                                                       \
-    if (cpl == 4) f32 ? launch_pstream_kv<KK, true, 4>(a, s) : launch_pstream_kv<KK, false, 4>(a, s); \
-    else f32 ? launch_pstream_kv<KK, true, 2>(a, s) : launch_pstream_kv<KK, false, 2>(a, s);          \
+#define H2D_CASE(KK)                                                                                               \
+  case KK:                                                                                                         \
+    if (cpl == 4) f32 ? launch_pstream_kv<KK, true, 4>(blk, d, pp, s) : launch_pstream_kv<KK, false, 4>(blk, d, pp, s); \
+    else f32 ? launch_pstream_kv<KK, true, 2>(blk, d, pp, s) : launch_pstream_kv<KK, false, 2>(blk, d, pp, s);          \
     break;
     H2D_PK_LIST(H2D_CASE)
 #undef H2D_CASE
@@ -581,10 +590,11 @@ int pstream_blocks_per_cu(int K, int precision, int cpl) {
 }
 
 void warm_pstream_kernels(int precision, int kmax, hipStream_t s) {
-  PStreamArgs a{};
-  a.nunits = 0;
+  static_assert(sizeof(PStreamArgs) <= kZeroArgBytes, "the zero block covers the persistent arguments");
+  const PStreamArgs* z = static_cast<const PStreamArgs*>(zero_arg_block());  // nunits 0: every wave exits
+  PStreamDyn d;
   for (int K = 1; K <= std::min(kmax, kMaxPK); ++K)
-    for (int cpl : {4, 2}) launch_pstream(a, K, precision, cpl, s);
+    for (int cpl : {4, 2}) launch_pstream(z, d, K, precision, cpl, false, s);
 }
 
 std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x, bool per_y, double row_edge_weight,
@@ -694,14 +704,15 @@ std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x
 }
 
 void warm_stream_kernels(int precision, int kmax, hipStream_t s) {
-  StreamArgs a{};
-  a.nunits = 0;
+  static_assert(sizeof(StreamArgs) <= kZeroArgBytes, "the zero block covers the streaming arguments");
+  const StreamArgs* z = static_cast<const StreamArgs*>(zero_arg_block());  // nunits 0: every wave exits
+  StreamDyn d;
   const bool f32 = precision == kFp32;
   for (int K = 1; K <= std::min(kmax, kMaxK); ++K) {
     if (!stream_k_supported(K)) continue;
     for (bool resid : {false, true}) {
       switch (K) {
-#define H2D_CASE(KK) case KK: launch_stream_k<KK>(a, f32, resid, s); break;
+#define H2D_CASE(KK) case KK: launch_stream_k<KK>(z, d, false, f32, resid, s); break;
         H2D_K_LIST(H2D_CASE)
 #undef H2D_CASE
         default: break;
@@ -819,5 +830,102 @@ void launch_lds_solver(const float* in, int64_t in_pitch, float* out, int64_t ou
                        sensitivity, steps_done, residual);
   H2D_HIP_CHECK(hipGetLastError());
 }
+
+
+// ---- device-resident kernel-argument blocks (ArgBlocks, kernels.h) ----------------------------
+namespace {
+// One wave copies a block from its pinned host slab into device memory: the stores go through
+// the L2 that the stencil kernels' scalar loads read (kernel boundaries order them), unlike a
+// DMA copy, which writes around the L2.
+__global__ __launch_bounds__(64) void arg_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16) {
+  for (int i = (int)threadIdx.x; i < n16; i += 64) dst[i] = src[i];
+}
+constexpr size_t kArgAlign = 256;       // blocks never share a cache line
+constexpr size_t kArgSlab = 64 * 1024;  // bytes per slab (more for a larger block)
+}  // namespace
+
+unsigned next_arg_tag() {
+  static std::atomic<unsigned> seq{0};
+  unsigned t = ++seq;
+  if (t == 0u) t = ++seq;
+  return t;
+}
+
+const void* zero_arg_block() {
+  static std::mutex mu;
+  static std::map<int, void*> blocks;  // per device, never freed (process lifetime)
+  int dev = 0;
+  H2D_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  void*& p = blocks[dev];
+  if (p == nullptr) {
+    H2D_HIP_CHECK(hipMalloc(&p, kZeroArgBytes));
+    H2D_HIP_CHECK(hipMemset(p, 0, kZeroArgBytes));
+    H2D_HIP_CHECK(hipDeviceSynchronize());
+  }
+  return p;
+}
+
+ArgBlocks::~ArgBlocks() { clear(); }
+
+void ArgBlocks::clear() {
+  for (Slab& sl : slabs_) {
+    if (sl.dev) hipFree(sl.dev);
+    if (sl.host) hipHostFree(sl.host);
+  }
+  slabs_.clear();
+  index_.clear();
+  n_blocks_ = n_bytes_ = 0;
+}
+
+const void* ArgBlocks::get_raw(const void* p, size_t n, ArgHead* head, hipStream_t s) {
+  if (n <= sizeof(ArgHead)) throw std::invalid_argument("ArgBlocks: empty argument block");
+  const char* c = static_cast<const char*>(p);
+  // the content after the header, and the size (blocks of different types never match)
+  std::string key(c + sizeof(ArgHead), n - sizeof(ArgHead));
+  key.append(reinterpret_cast<const char*>(&n), sizeof n);
+  auto it = index_.find(key);
+  if (it != index_.end()) {
+    Entry& e = it->second;
+    if (!e.ready && e.stream != s) {
+      // first use on another stream: the upload (a kernel on its stream) must have completed
+      H2D_HIP_CHECK(hipStreamSynchronize(e.stream));
+      e.ready = true;
+    }
+    head->btag = e.tag;
+    head->bytes = (unsigned)n;
+    return e.dev;
+  }
+  const size_t need = (n + kArgAlign - 1) / kArgAlign * kArgAlign;
+  if (slabs_.empty() || slabs_.back().used + need > slabs_.back().cap) {
+    Slab sl;
+    sl.cap = std::max(kArgSlab, need);
+    H2D_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&sl.dev), sl.cap));
+    if (hipHostMalloc(reinterpret_cast<void**>(&sl.host), sl.cap, hipHostMallocDefault) != hipSuccess) {
+      hipFree(sl.dev);
+      throw std::runtime_error("ArgBlocks: hipHostMalloc failed");
+    }
+    std::memset(sl.host, 0, sl.cap);
+    slabs_.push_back(sl);
+  }
+  Slab& sl = slabs_.back();
+  head->btag = next_arg_tag();
+  head->bytes = (unsigned)n;
+  char* h = sl.host + sl.used;
+  char* d = sl.dev + sl.used;
+  std::memcpy(h, p, n);  // (the rest of the aligned span stays zero)
+  void* hd = nullptr;
+  H2D_HIP_CHECK(hipHostGetDevicePointer(&hd, h, 0));
+  hipLaunchKernelGGL(arg_copy_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const uint4*>(hd),
+                     reinterpret_cast<uint4*>(d), (int)(need / 16));
+  H2D_HIP_CHECK(hipGetLastError());
+  sl.used += need;
+  ++n_blocks_;
+  ++n_uploads_;
+  n_bytes_ += need;
+  index_.emplace(std::move(key), Entry{d, head->btag, s, false});
+  return d;
+}
+
 
 }  // namespace h2d

@@ -97,8 +97,8 @@ __device__ __forceinline__ bool pensure(PSlot& d, int A, int B, unsigned cprev, 
     d.known = max(d.known, v);
     if (__ballot(nd > d.known) == 0ull) return true;
     if (i > a.halo_polls ||
-        ((i & 63) == 63 && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
-      if (__lane_id() == 0) report_timeout(a.timed_out, a.timed_out_host, 8u);
+        ((i & 63) == 63 && __hip_atomic_load(gp(a.timed_out), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+      if (__lane_id() == 0) report_timeout(gp(a.timed_out), gp(a.timed_out_host), 8u);
       dead = true;
       return false;
     }
@@ -117,15 +117,23 @@ __device__ __forceinline__ void ppublish(unsigned* p, unsigned v, int lane) {
 // ever counts whole chunks.
 __device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int lane, unsigned long long* lsig,
                                         unsigned long long lneed, const PStreamArgs& a, bool& dead) {
-  if (lsig != nullptr && lane == 0 && !dead) {
-    long long i = 0;
-    while (__hip_atomic_load(lsig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < lneed) {
-      if (++i > a.halo_polls) {
-        report_timeout(a.timed_out, a.timed_out_host, 8u);
-        break;
+  if (lsig != nullptr && !dead) {
+    int gave_up = 0;
+    if (lane == 0) {
+      long long i = 0;
+      while (__hip_atomic_load(lsig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < lneed) {
+        // bounded; and a wait that failed elsewhere in the engine ends this one too (fail fast:
+        // one failure must not cost every later chunk's signal a full timeout)
+        if (++i > a.halo_polls ||
+            ((i & 63) == 0 && __hip_atomic_load(gp(a.timed_out), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+          report_timeout(gp(a.timed_out), gp(a.timed_out_host), 8u);
+          gave_up = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_s_sleep(1);
     }
+    if (__builtin_amdgcn_readfirstlane(gave_up) != 0) dead = true;
   }
   if (rel == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   else if (rel == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -138,8 +146,9 @@ __device__ __forceinline__ void psignal(unsigned long long* sig, int rel, int la
 
 // PUSH: a direct-pipeline halo unit (copies its first rows to the neighbour GPU each chunk); the
 // other units' steady loop carries no per-row push check.
-template <int K, bool F32, int EDGE, bool FIXED, int CPL, bool PUSH>
-__device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w, int lane, PSlot& sl) {
+template <int K, bool F32, int EDGE, bool FIXED, int CPL, bool PUSH, bool PP>
+__device__ __forceinline__ void prun(const PStreamArgs& a, const PStreamDyn& d, const Unit& u, int w, int lane,
+                                     PSlot& sl) {
   typedef typename LaneVec<CPL>::T V;
   // rows per steady iteration (8 for 2-column lanes was measured slower: 512x4096 K=8 2.21 vs
   // 1.91 us/step — its rows are published an iteration later, so the neighbours start later)
@@ -162,7 +171,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   const int64_t xout = rev ? x0 + h - 1 : x0;
   const int pb = (int)(a.pitch * (int64_t)sizeof(float));  // row bytes (the host keeps n * pb < 2^31)
   const Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
-  unsigned* myprog = a.prog + 32 * w;
+  unsigned* myprog = gp(a.prog) + 32 * w;
 
   // chunk-invariant lane context (stream_kernel's, write-through stores, no residual / sides)
   LaneCtx c;
@@ -179,13 +188,13 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   c.m2 = CPL > 2 && colmask(gc + 2);
   c.m3 = CPL > 2 && colmask(gc + 3);
   const bool in_out = (cb >= u.olo) && (cb < u.ohi);
-  c.sout = a.dummy + CPL * lane;  // unused: write-through path
+  c.sout = gp(a.dummy) + CPL * lane;  // unused: write-through path
   c.spitch = 0;
   c.obs = rev ? -pb : pb;
   c.obo = rev ? (h - 1) * pb : 0;
   c.voff = in_out ? 4u * CPL * (unsigned)lane : 0x80000000u;
   c.st0 = c.st1 = c.st2 = c.st3 = false;
-  c.kout = a.dummy + CPL * lane;
+  c.kout = gp(a.dummy) + CPL * lane;
   c.kpitch = 0;
   c.rel = a.rel;
   c.spu = false;
@@ -199,16 +208,16 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   // direction-resolved halo pointers: selects, not runtime-indexed kernel-argument arrays (a
   // runtime index into the argument block made hipcc copy the whole block to scratch and reload
   // fields from it at every iteration top)
-  const unsigned long long* const waitd = rev ? a.wait[1] : a.wait[0];
-  const unsigned long long need0 = rev ? a.need0[1] : a.need0[0];
+  const unsigned long long* const waitd = rev ? gp(a.wait[1]) : gp(a.wait[0]);
+  const unsigned long long need0 = rev ? d.need0[1] : d.need0[0];
   const unsigned long long needinc = rev ? a.need_inc[1] : a.need_inc[0];
-  const float* const hsrc0 = rev ? a.hsrc[1][0] : a.hsrc[0][0];
-  const float* const hsrc1 = rev ? a.hsrc[1][1] : a.hsrc[0][1];
-  float* const push0 = rev ? a.push[1][0] : a.push[0][0];
-  float* const push1 = rev ? a.push[1][1] : a.push[0][1];
-  unsigned long long* const sigd = rev ? a.sig[1] : a.sig[0];
-  unsigned long long* const lsigd = rev ? a.lsig[1] : a.lsig[0];
-  const unsigned long long lbased = rev ? a.lbase[1] : a.lbase[0];
+  const float* const hsrc0 = rev ? gp(a.hsrc[1][0]) : gp(a.hsrc[0][0]);
+  const float* const hsrc1 = rev ? gp(a.hsrc[1][1]) : gp(a.hsrc[0][1]);
+  float* const push0 = rev ? gp(a.push[1][0]) : gp(a.push[0][0]);
+  float* const push1 = rev ? gp(a.push[1][1]) : gp(a.push[0][1]);
+  unsigned long long* const sigd = rev ? gp(a.sig[1]) : gp(a.sig[0]);
+  unsigned long long* const lsigd = rev ? gp(a.lsig[1]) : gp(a.lsig[0]);
+  const unsigned long long lbased = rev ? d.lbase[1] : d.lbase[0];
   const unsigned long long lperd = (unsigned long long)(rev ? a.lper[1] : a.lper[0]);
   const bool pushes = PUSH && ns && push0 != nullptr;
   c.prows = pushes ? a.sig_rows : 0;
@@ -227,7 +236,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   // an untaken runtime branch per iteration top cost ~30 % at 512x4096: the timers' registers
   // and the loop's scheduling)
 #ifdef H2D_PSTREAM_PHASES
-  const bool tm = a.phase != nullptr;
+  const bool tm = gp(a.phase) != nullptr;
   unsigned long long ph[kPhases] = {};
   unsigned long long tq = tm ? __builtin_amdgcn_s_memrealtime() : 0ull;
   auto lap = [&](int i) {
@@ -240,17 +249,17 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
 #else
   auto lap = [](int) {};
 #endif
-  for (int j = 0; j < a.nchunks; ++j) {
-    const unsigned cidx = a.cbase + (unsigned)j;
-    const int par = (a.cur0 + j) & 1;
-    const float* src = par ? a.buf[1] : a.buf[0];
-    float* dst = par ? a.buf[0] : a.buf[1];
-    const int ipar = (a.ipar0 + j) & 1;
+  for (int j = 0; j < d.nchunks; ++j) {
+    const unsigned cidx = d.cbase + (unsigned)j;
+    const int par = (d.cur0 + j) & 1;
+    const float* src = par ? gp(a.buf[1]) : gp(a.buf[0]);
+    float* dst = par ? gp(a.buf[0]) : gp(a.buf[1]);
+    const int ipar = (d.ipar0 + j) & 1;
     if (j > 0) {
       // chunk start: my previous chunk's stores complete (the poll's wait drains them), publish
       // them, then the rows the up-front batch loads must be published by the neighbours
       lap(5);
-      const unsigned pv = ppoll(sl, a.prog);
+      const unsigned pv = ppoll(sl, gp(a.prog));
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       ppublish(myprog, cidx * (unsigned)h, lane);
       if (sig_pending) {
@@ -259,28 +268,28 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       }
       sl.known = max(sl.known, pv);
       lap(1);
-      pensure(sl, 0, min(n, 2 * K + RI), cidx - 1u, a.prog, a, dead);
+      pensure(sl, 0, min(n, 2 * K + RI), cidx - 1u, gp(a.prog), a, dead);
       lap(2);
     }
     const V* hrowp = nullptr;
     if (ns && waitd != nullptr) {
       // the neighbour GPU's pushes of its chunk j-1 (this chunk's ghost rows)
-      if (lane == 0 && !dead && __hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+      if (lane == 0 && !dead && __hip_atomic_load(gp(a.timed_out), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
         const unsigned long long need = need0 + (unsigned long long)j * needinc;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         long long i = 0;
         while (__hip_atomic_load(waitd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
           if (++i > a.halo_polls) {
-            report_timeout(a.timed_out, a.timed_out_host, 2u);
+            report_timeout(gp(a.timed_out), gp(a.timed_out_host), 2u);
             break;
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        if (a.wait_acc != nullptr) {
+        if (gp(a.wait_acc) != nullptr) {
           const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
-          __hip_atomic_fetch_add(a.wait_acc, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(a.wait_acc + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_max(a.wait_acc + 2, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(gp(a.wait_acc), dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(gp(a.wait_acc) + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_max(gp(a.wait_acc) + 2, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       if (a.acq == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -290,7 +299,7 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
       lap(3);
     }
     c.obase = dst + out_base;
-    c.pout = (pushes && in_out) ? (ipar ? push0 : push1) + xout * a.pitch + a.PL + cb : a.dummy + CPL * lane;
+    c.pout = (pushes && in_out) ? (ipar ? push0 : push1) + xout * a.pitch + a.PL + cb : gp(a.dummy) + CPL * lane;
     c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
     const __amdgpu_buffer_rsrc_t rin =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src) + in_base, (short)0, n * pb, 0x00020000);
@@ -317,43 +326,82 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
     bool signalled = false;
     unsigned polled = 0u;
     bool have_poll = false;
+    int it = 0;
+    // One publishing top per RI rows: every op issued before the previous top has completed
+    // (>= 8 VMEM ops since), so the progress word and the halo signal can go out, the neighbours'
+    // words are polled (consumed at the next top), and the rows this iteration's loads need are
+    // ensured.
+#define H2D_PTOP()                                                                                \
+  {                                                                                               \
+    lap(5);                                                                                       \
+    if (PE == 1 || (it++ % PE) == 0) {                                                            \
+      if constexpr (RI == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");                    \
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                                       \
+      ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);                         \
+      if (pushes && !signalled && issued_prev >= a.sig_rows) { /* the pushed rows have completed */ \
+        psignal(sigd, a.rel, lane, lsigd, lbased + (unsigned long long)j * lperd, a, dead);       \
+        signalled = true;                                                                         \
+      }                                                                                           \
+      if (have_poll) sl.known = max(sl.known, polled);                                            \
+      polled = ppoll(sl, gp(a.prog));                                                             \
+      have_poll = true;                                                                           \
+    }                                                                                             \
+    issued_prev = ir0 - 2 * K;                                                                    \
+    if (j > 0) pensure(sl, ir0 + RI, min(n, ir0 + 2 * RI), cidx - 1u, gp(a.prog), a, dead);       \
+    lap(6);                                                                                       \
+  }
+    if constexpr (!PP) {
+      // each row's replacement is loaded as the row is consumed (loop-carried register copies)
 #define H2D_PSTEADY(D)                                                                \
   {                                                                                   \
     const V nw = pf[D];                                                               \
     pf[D] = load_row_sc1<V>(rin, lvoff, soff(min(ir0 + (D) + RI, n - 1)));            \
     process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, (D)&1, K>(S, nw, ir0 + (D), c, k, racc); \
   }
-    int it = 0;
-    for (; ir0 + RI <= n; ir0 += RI) {
-      lap(5);
-      if (PE == 1 || (it++ % PE) == 0) {
-        // publishing top: every op before the previous top has completed (>= 8 VMEM ops since)
-        if constexpr (RI == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        ppublish(myprog, cidx * (unsigned)h + (unsigned)issued_prev, lane);
-        if (pushes && !signalled && issued_prev >= a.sig_rows) {  // the pushed rows have completed
-          psignal(sigd, a.rel, lane, lsigd, lbased + (unsigned long long)j * lperd, a, dead);
-          signalled = true;
+      for (; ir0 + RI <= n; ir0 += RI) {
+        H2D_PTOP()
+        H2D_PSTEADY(0)
+        H2D_PSTEADY(1)
+        H2D_PSTEADY(2)
+        H2D_PSTEADY(3)
+        if constexpr (RI == 8) {
+          H2D_PSTEADY(4)
+          H2D_PSTEADY(5)
+          H2D_PSTEADY(6)
+          H2D_PSTEADY(7)
         }
-        if (have_poll) sl.known = max(sl.known, polled);
-        polled = ppoll(sl, a.prog);  // consumed at the next publishing top
-        have_poll = true;
       }
-      issued_prev = ir0 - 2 * K;
-      if (j > 0) pensure(sl, ir0 + RI, min(n, ir0 + 2 * RI), cidx - 1u, a.prog, a, dead);
-      lap(6);
-      H2D_PSTEADY(0)
-      H2D_PSTEADY(1)
-      H2D_PSTEADY(2)
-      H2D_PSTEADY(3)
-      if constexpr (RI == 8) {
-        H2D_PSTEADY(4)
-        H2D_PSTEADY(5)
-        H2D_PSTEADY(6)
-        H2D_PSTEADY(7)
-      }
-    }
 #undef H2D_PSTEADY
+    } else {
+      // ping-pong: the next RI rows are loaded right after the top, a whole iteration ahead of
+      // their use, into the register set the previous iteration consumed (as the streaming
+      // kernel): no loop-carried register copies, whose waits drained the row stores too
+#define H2D_PROW(CUR, D) \
+  process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, (D)&1, K>(S, CUR[D], ir0 + (D), c, k, racc);
+#define H2D_PITER(CUR, NXT)                                                         \
+  {                                                                                 \
+    H2D_PTOP()                                                                      \
+    _Pragma("unroll") for (int d = 0; d < RI; ++d)                                  \
+        NXT[d] = load_row_sc1<V>(rin, lvoff, soff(min(ir0 + d + RI, n - 1)));       \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    H2D_PROW(CUR, 0) H2D_PROW(CUR, 1) H2D_PROW(CUR, 2) H2D_PROW(CUR, 3)             \
+    if constexpr (RI == 8) { H2D_PROW(CUR, 4) H2D_PROW(CUR, 5) H2D_PROW(CUR, 6) H2D_PROW(CUR, 7) } \
+    ir0 += RI;                                                                      \
+  }
+      V nx[RI];
+      while (ir0 + 2 * RI <= n) {
+        H2D_PITER(pf, nx)
+        H2D_PITER(nx, pf)
+      }
+      if (ir0 + RI <= n) {
+        H2D_PITER(pf, nx)
+#pragma unroll
+        for (int d = 0; d < RI; ++d) pf[d] = nx[d];
+      }
+#undef H2D_PITER
+#undef H2D_PROW
+    }
+#undef H2D_PTOP
     if (ir0 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 0, K>(S, pf[0], ir0, c, k, racc);
     if (ir0 + 1 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 1, K>(S, pf[1], ir0 + 1, c, k, racc);
     if (ir0 + 2 < n) process_row<K, F32, EDGE, FIXED, false, true, false, PUSH, 0, K>(S, pf[2], ir0 + 2, c, k, racc);
@@ -372,25 +420,48 @@ __device__ __forceinline__ void prun(const PStreamArgs& a, const Unit& u, int w,
   }
   lap(5);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  ppublish(myprog, (a.cbase + (unsigned)a.nchunks) * (unsigned)h, lane);
+  ppublish(myprog, (d.cbase + (unsigned)d.nchunks) * (unsigned)h, lane);
   if (sig_pending) psignal(sigd, a.rel, lane, lsigd, lbased + (unsigned long long)sig_chunk * lperd, a, dead);
   lap(1);
 #ifdef H2D_PSTREAM_PHASES
   if (tm && lane == 0) {
-    ph[0] = (unsigned long long)a.nchunks;
+    ph[0] = (unsigned long long)d.nchunks;
 #pragma unroll
-    for (int i = 0; i < kPhases; ++i) __hip_atomic_fetch_add(a.phase + i, ph[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < kPhases; ++i) __hip_atomic_fetch_add(gp(a.phase) + i, ph[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #endif
 }
 
-template <int K, bool F32, int CPL>
-__global__ __launch_bounds__(256) void pstream_kernel(PStreamArgs a) {
+// The per-launch values arrive as scalar kernel arguments; prun sees them as a PStreamDyn.  PP: the
+// ping-pong steady loop.
+template <int K, bool F32, int CPL, bool PP>
+__global__ __launch_bounds__(256) void pstream_kernel(const PStreamArgs* __restrict__ ap, unsigned long long need0n,
+                                                      unsigned long long need0s, unsigned long long lbasen,
+                                                      unsigned long long lbases, unsigned cbase, int nchunks,
+                                                      int parities, unsigned btag) {
+  // (read once, up front: see stream_kernel)
+  asm volatile("" : "+s"(need0n), "+s"(need0s), "+s"(lbasen), "+s"(lbases), "+s"(cbase), "+s"(nchunks),
+               "+s"(parities), "+s"(btag));
+  PStreamDyn d;
+  d.nchunks = nchunks;
+  d.cbase = cbase;
+  d.cur0 = parities & 1;
+  d.ipar0 = (parities >> 1) & 1;
+  d.btag = btag;
+  d.need0[0] = need0n;
+  d.need0[1] = need0s;
+  d.lbase[0] = lbasen;
+  d.lbase[1] = lbases;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int w = (int)blockIdx.x * 4 + wv;
+  const PStreamArgs& a = *ap;  // the plan's immutable device-resident block (zero_arg_block: no-op)
   if (w >= a.nunits) return;
   const int lane = (int)(threadIdx.x & 63);
-  const PUnit* pu = a.units + w;
+  if (a.head.btag != d.btag) {  // a block the launch does not name: report, compute nothing
+    if (lane == 0) report_timeout(gp(a.timed_out), gp(a.timed_out_host), kIntegArgs);
+    return;
+  }
+  const PUnit* pu = gp(a.units) + w;
   const Unit u = pu->u;
   PSlot sl;
   if (lane < kPSlots) {
@@ -411,18 +482,18 @@ __global__ __launch_bounds__(256) void pstream_kernel(PStreamArgs a) {
   // us/step, 512x4096 2.21 vs 2.11: the publishing top's counted vmcnt waits on a steady loop
   // whose stores the scheduler had moved later)
   switch (u.flags & 3) {
-    case 0: prun<K, F32, 0, false, CPL, true>(a, u, w, lane, sl); break;
+    case 0: prun<K, F32, 0, false, CPL, true, PP>(a, d, u, w, lane, sl); break;
     case 1:
-      if (fixed) prun<K, F32, 1, true, CPL, true>(a, u, w, lane, sl);
-      else prun<K, F32, 1, false, CPL, true>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 1, true, CPL, true, PP>(a, d, u, w, lane, sl);
+      else prun<K, F32, 1, false, CPL, true, PP>(a, d, u, w, lane, sl);
       break;
     case 2:
-      if (fixed) prun<K, F32, 2, true, CPL, true>(a, u, w, lane, sl);
-      else prun<K, F32, 2, false, CPL, true>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 2, true, CPL, true, PP>(a, d, u, w, lane, sl);
+      else prun<K, F32, 2, false, CPL, true, PP>(a, d, u, w, lane, sl);
       break;
     default:
-      if (fixed) prun<K, F32, 3, true, CPL, true>(a, u, w, lane, sl);
-      else prun<K, F32, 3, false, CPL, true>(a, u, w, lane, sl);
+      if (fixed) prun<K, F32, 3, true, CPL, true, PP>(a, d, u, w, lane, sl);
+      else prun<K, F32, 3, false, CPL, true, PP>(a, d, u, w, lane, sl);
       break;
   }
 }
@@ -430,15 +501,18 @@ __global__ __launch_bounds__(256) void pstream_kernel(PStreamArgs a) {
 }  // namespace
 
 template <int K, bool F32, int CPL>
-void launch_pstream_kv(const PStreamArgs& a, hipStream_t s) {
-  const int blocks = std::max(1, (a.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_pstream_kernels)
-  hipLaunchKernelGGL((pstream_kernel<K, F32, CPL>), dim3(blocks), dim3(256), 0, s, a);
+void launch_pstream_kv(const PStreamArgs* blk, const PStreamDyn& d, bool pingpong, hipStream_t s) {
+  const int blocks = std::max(1, (d.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_pstream_kernels)
+  void (*fn)(const PStreamArgs*, unsigned long long, unsigned long long, unsigned long long, unsigned long long,
+             unsigned, int, int, unsigned) = pingpong ? pstream_kernel<K, F32, CPL, true> : pstream_kernel<K, F32, CPL, false>;
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, blk, d.need0[0], d.need0[1], d.lbase[0], d.lbase[1], d.cbase,
+                     d.nchunks, (d.cur0 & 1) | ((d.ipar0 & 1) << 1), d.btag);
 }
 
 template <int K, bool F32, int CPL>
 int pstream_blocks_per_cu_v() {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(pstream_kernel<K, F32, CPL>),
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(pstream_kernel<K, F32, CPL, false>),
                                                    256, 0) != hipSuccess)
     return 0;
   return nb;

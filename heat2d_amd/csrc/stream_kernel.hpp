@@ -34,6 +34,17 @@
 namespace h2d {
 namespace {
 
+// A pointer read from a device-resident argument block is generic (flat) to the compiler; every
+// buffer the kernels touch — tiles, unit lists, peer memory mapped over xGMI, host-mapped words —
+// lies in the global aperture, so say so: global_load / global_store instead of flat (in-order
+// completion for the counted vmcnt waits, no lgkmcnt on every wait, and a buffer resource built
+// from a uniform base instead of a readfirstlane waterfall per store).
+// (Through an integer: an addrspacecast round trip generic -> global -> generic folds away.)
+template <class T>
+__device__ __forceinline__ T* gp(T* p) {
+  return (T*)(__attribute__((address_space(1))) T*)(uintptr_t)p;
+}
+
 // lane i <- lane i-1 (DPP wave_shr:1), lane i <- lane i+1 (DPP wave_shl:1).
 // bound_ctrl=1 (lanes without a source read 0, the add identity) lets the compiler fold the
 // DPP move into the consuming v_add_f32 (one VALU op instead of two).
@@ -499,13 +510,13 @@ __device__ __forceinline__ void run_plain(const Unit& u, const float4* rowp, con
 
 // The decision of a convergence check, by the one lane that holds the total.
 __device__ __forceinline__ void decide_total(double r, const DecideArgs& d) {
-  if (*d.stop != 0ull) return;  // already stopped
-  __hip_atomic_store(&d.host->last, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&d.host->checks, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (*gp(d.stop) != 0ull) return;  // already stopped
+  __hip_atomic_store(&gp(d.host)->last, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&gp(d.host)->checks, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (r < d.sens) {
-    *d.stop = d.seq;
-    __hip_atomic_store(&d.host->residual, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&d.host->stop_seq, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    *gp(d.stop) = d.seq;
+    __hip_atomic_store(&gp(d.host)->residual, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&gp(d.host)->stop_seq, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -516,10 +527,10 @@ __device__ __forceinline__ void decide_total(double r, const DecideArgs& d) {
 __device__ __forceinline__ void publish_partial(double* partials, int slot, double v, int nparts,
                                                 const DecideArgs& d, int lane) {
   if (lane == 0) __hip_atomic_store(partials + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (d.ticket == nullptr) return;
+  if (gp(d.ticket) == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int last = 0;
-  if (lane == 0) last = __hip_atomic_fetch_add(d.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+  if (lane == 0) last = __hip_atomic_fetch_add(gp(d.ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                         (unsigned)(nparts - 1);
   last = __shfl(last, 0, 64);
   if (!last) return;
@@ -528,64 +539,91 @@ __device__ __forceinline__ void publish_partial(double* partials, int slot, doub
   for (int i = lane; i < nparts; i += 64) s += __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   s = wave_sum(s);
   if (lane == 0) {
-    *d.total = s;
-    if (d.host != nullptr) decide_total(s, d);  // else a cross-tile / cross-rank sum decides later
-    __hip_atomic_store(d.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *gp(d.total) = s;
+    if (gp(d.host) != nullptr) decide_total(s, d);  // else a cross-tile / cross-rank sum decides later
+    __hip_atomic_store(gp(d.ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 template <int K, bool F32, bool RESID, bool WT>
-__global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
+__global__ __launch_bounds__(256) void stream_kernel(const StreamArgs* __restrict__ ap, unsigned long long lid_arg,
+                                                     unsigned long long copies_need_arg, unsigned long long seq_arg,
+                                                     unsigned btag_arg, StreamNeed need) {
+  // The per-launch scalars sit in kernel-argument memory (host memory, the library's default):
+  // read once, up front, in the block pointer's batch, and kept in SGPRs — the asm makes them
+  // values, not loads the compiler may repeat (a host round trip each) later in the wave.
+  unsigned long long lid = lid_arg, copies_need = copies_need_arg, seq = seq_arg;
+  unsigned btag = btag_arg;
+  asm volatile("" : "+s"(lid), "+s"(copies_need), "+s"(seq), "+s"(btag));
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int w = (int)blockIdx.x * 4 + wv;
-  if (w >= a.nunits) return;
+  // the plan's arguments: an immutable device-resident block (scalar loads, L2 / K$ resident).
+  // No-op launches (warm_stream_kernels) pass the zero block (zero_arg_block: nunits 0).
+  const StreamArgs& a = *ap;
+  // the block fields the preamble needs, loaded as ONE batch (one wait instead of a chain of
+  // dependent round trips behind each early-exit test)
+  // (the unit-list pointer stays a plain block load: the unit's own load must remain scalar)
+  int nunits = a.nunits, nsignal = a.nsignal;
+  const unsigned long long* stamps_p = gp(a.stamps);
+  asm volatile("" : "+s"(nunits), "+s"(nsignal), "+s"(stamps_p));
+  if (w >= nunits) return;
   const int lane = (int)(threadIdx.x & 63);
-  const bool stamping = a.stamps != nullptr;  // diagnostics: per-wave timeline
+  const bool stamping = stamps_p != nullptr;  // diagnostics: per-wave timeline
   const unsigned long long t_start = stamping ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  const Unit u = a.units[w];
-  if (a.lid != 0ull) {
-    // integrity (wave-uniform, scalar): both ends of the argument block name this launch, the
-    // unit comes from the list the launch names, and (serial pipeline) the exchange copy in
-    // front of this launch has finished — else report and compute nothing
-    unsigned bad = a.lid_tail != a.lid ? kIntegArgs : u.tag != a.utag ? kIntegUnits : 0u;
-    if (bad == 0u && w == 0 && a.copies_done != nullptr &&
-        __hip_atomic_load(a.copies_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.copies_need)
+  const Unit u = gp(a.units)[w];
+  const bool halo_unit = w < nsignal;
+  const bool ns_unit = halo_unit && (u.flags & kUnitNS) != 0;  // top / bottom halo unit of its strip
+  const int dir = (u.flags & kUnitReverse) ? 1 : 0;  // 0: north halo (top unit), 1: south (bottom unit)
+  const int xreads = halo_unit ? (u.links & 0x3f) : 0;          // 2-D direct: side ghosts read
+  const int xpushes = halo_unit ? ((u.links >> 8) & 0x3f) : 0;  // 2-D direct: sides pushed to
+  // A wave that does no work still counts: its halo signals, so gates and flags of launches
+  // already queued on other streams and ranks stay in step (and a failed launch is reported by
+  // the host's poll instead of a neighbour's wait running into its timeout), and its serial-
+  // pipeline wave count.
+  auto skip_unit = [&]() {
+    if (ns_unit && gp(a.sig[dir]) != nullptr && lane == 0)
+      __hip_atomic_fetch_add(gp(a.sig[dir]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0)
+      for (int i = 0; i < kSideLinks; ++i)
+        if ((xpushes >> i) & 1) __hip_atomic_fetch_add(gp(a.xsig[i]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0 && gp(a.waves_done) != nullptr)
+      __hip_atomic_fetch_add(gp(a.waves_done), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (lid != 0ull) {
+    // integrity (wave-uniform, scalar): the launch names this block, the unit comes from the
+    // list the block names, and (serial pipeline) the exchange copy in front of this launch has
+    // finished — else report and skip
+    unsigned bad = a.head.btag != btag ? kIntegArgs : u.tag != a.utag ? kIntegUnits : 0u;
+    if (bad == 0u && w == 0 && gp(a.copies_done) != nullptr &&
+        __hip_atomic_load(gp(a.copies_done), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != copies_need)
       bad = kIntegOrder;
     if (bad != 0u) {
-      if (lane == 0) report_timeout(a.timed_out, a.timed_out_host, bad);
-      if (lane == 0 && a.waves_done != nullptr)
-        __hip_atomic_fetch_add(a.waves_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) report_timeout(gp(a.timed_out), gp(a.timed_out_host), bad);
+      skip_unit();
       return;
     }
   }
   // replay check: launch ids rise in stream order, so an older or equal id seen already means this
   // launch ran with the arguments of an earlier one.  Issued here, its value is checked at the
   // wave's end (the atomic's round trip overlaps the work instead of delaying the launch's end).
+  // Every other wave reads the highest id seen: engine launches all run in order on one stream,
+  // so a wave whose per-launch part names an id below it ran with an older launch's arguments
+  // (a wave of the same launch may have raised it to lid already; an older id never passes).
   unsigned long long lid_old = 0ull;
-  const bool replay_check = w == 0 && lane == 0 && a.lid != 0ull && a.lid_seen != nullptr;
-  if (replay_check) lid_old = __hip_atomic_fetch_max(a.lid_seen, a.lid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const bool halo_unit = w < a.nsignal;
-  const bool ns_unit = halo_unit && (u.flags & kUnitNS) != 0;  // top / bottom halo unit of its strip
-  const int dir = (u.flags & kUnitReverse) ? 1 : 0;  // 0: north halo (top unit), 1: south (bottom unit)
-  const int xreads = halo_unit ? (u.links & 0x3f) : 0;          // 2-D direct: side ghosts read
-  const int xpushes = halo_unit ? ((u.links >> 8) & 0x3f) : 0;  // 2-D direct: sides pushed to
-  if (a.stop != nullptr && __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) {
-    // converged earlier in this run: no work, but halo units still count, so gates / flags of
-    // launches already queued on other streams and ranks stay in step
-    if (ns_unit && a.sig[dir] != nullptr && lane == 0)
-      __hip_atomic_fetch_add(a.sig[dir], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (lane == 0)
-      for (int i = 0; i < kSideLinks; ++i)
-        if ((xpushes >> i) & 1) __hip_atomic_fetch_add(a.xsig[i], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (lane == 0 && a.waves_done != nullptr)
-      __hip_atomic_fetch_add(a.waves_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool replay_check = lane == 0 && lid != 0ull && gp(a.lid_seen) != nullptr;
+  if (replay_check) {
+    if (w == 0) lid_old = __hip_atomic_fetch_max(gp(a.lid_seen), lid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else lid_old = __hip_atomic_load(gp(a.lid_seen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (gp(a.stop) != nullptr && __hip_atomic_load(gp(a.stop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) {
+    skip_unit();  // converged earlier in this run: no work
     return;
   }
-  const bool ns_wait = ns_unit && a.wait[dir] != nullptr;
+  const bool ns_wait = ns_unit && gp(a.wait[dir]) != nullptr;
   if (ns_wait || xreads != 0) {
     // wait until the exchange that fills this unit's ghost rows has landed (a wait that already
     // timed out in this engine stops every later wait: fail fast)
-    if (__hip_atomic_load(a.timed_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+    if (__hip_atomic_load(gp(a.timed_out), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       // every flag this unit needs is polled at once, one per lane (lanes 0-5: the side links,
       // lane 6: the N/S flag) — one round trip per poll, not one per flag; relaxed polls (an
@@ -595,28 +633,28 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
 #pragma unroll
       for (int x = 0; x < kSideLinks; ++x)
         if (lane == x && ((xreads >> x) & 1) != 0) {
-          wp = a.xwait[x];
-          wneed = a.xneed[x];
+          wp = gp(a.xwait[x]);
+          wneed = need.v[2 + x];
         }
       if (lane == kSideLinks && ns_wait) {
-        wp = a.wait[dir];
-        wneed = a.need[dir];
+        wp = gp(a.wait[dir]);
+        wneed = dir ? need.v[1] : need.v[0];
       }
       bool pending = wp != nullptr;
       for (long long i = 0;; ++i) {
         if (pending) pending = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < wneed;
         if (__ballot(pending) == 0ull) break;
         if (i >= a.halo_polls) {
-          if (lane == 0) report_timeout(a.timed_out, a.timed_out_host, 2u);
+          if (lane == 0) report_timeout(gp(a.timed_out), gp(a.timed_out_host), 2u);
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      if (a.wait_acc != nullptr && lane == 0) {  // exposed halo wait of this unit (fire-and-forget atomics)
+      if (gp(a.wait_acc) != nullptr && lane == 0) {  // exposed halo wait of this unit (fire-and-forget atomics)
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
-        __hip_atomic_fetch_add(a.wait_acc, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(a.wait_acc + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_max(a.wait_acc + 2, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(gp(a.wait_acc), dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(gp(a.wait_acc) + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(gp(a.wait_acc) + 2, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     // acq 0: system scope; 1: agent scope (this CU's L1); 2: the ghost rows are in uncached
@@ -651,10 +689,10 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   // Lanes in the output range store a full float4 (columns past ycell land in the ghost /
   // pad columns inside the pitch and hold valid cone values there); others hit a dummy slot.
   const bool in_out = (cb >= u.olo) && (cb < u.ohi);
-  float* out = a.dst + (a.G + xout) * a.pitch + a.PL + cb;
-  c.sout = in_out ? out : a.dummy + 4 * lane;
+  float* out = gp(a.dst) + (a.G + xout) * a.pitch + a.PL + cb;
+  c.sout = in_out ? out : gp(a.dummy) + 4 * lane;
   c.spitch = in_out ? (rev ? -a.pitch : a.pitch) : 0;
-  c.obase = a.dst + (a.G + x0) * a.pitch + a.PL + u.cb;
+  c.obase = gp(a.dst) + (a.G + x0) * a.pitch + a.PL + u.cb;
   c.obs = (int)((rev ? -a.pitch : a.pitch) * (int64_t)sizeof(float));
   c.obo = rev ? (h - 1) * (int)(a.pitch * (int64_t)sizeof(float)) : 0;
   c.voff = in_out ? 16u * (unsigned)lane : 0x80000000u;
@@ -662,13 +700,13 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   c.st1 = in_out && cb + 1 < a.ycell;
   c.st2 = in_out && cb + 2 < a.ycell;
   c.st3 = in_out && cb + 3 < a.ycell;
-  const bool pushes = ns_unit && a.push[dir] != nullptr;
+  const bool pushes = ns_unit && gp(a.push[dir]) != nullptr;
   c.prows = pushes ? a.sig_rows : 0;
   c.rel = a.rel;
-  const bool keeps = a.keep != nullptr && in_out;
-  c.kout = keeps ? a.keep + (out - a.dst) : a.dummy + 4 * lane;
+  const bool keeps = gp(a.keep) != nullptr && in_out;
+  c.kout = keeps ? gp(a.keep) + (out - gp(a.dst)) : gp(a.dummy) + 4 * lane;
   c.kpitch = keeps ? c.spitch : 0;
-  c.pout = (pushes && in_out) ? a.push[dir] + xout * a.pitch + a.PL + cb : a.dummy + 4 * lane;
+  c.pout = (pushes && in_out) ? gp(a.push[dir]) + xout * a.pitch + a.PL + cb : gp(a.dummy) + 4 * lane;
   c.ppitch = (pushes && in_out) ? (rev ? -a.pitch : a.pitch) : 0;
 
   // 2-D direct side pushes: this lane's elements in the W / E neighbour's halo columns
@@ -691,32 +729,32 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     const int64_t sgn = rev ? -1 : 1;
     if (c.em != 0u) {
       if ((xpushes >> side) & 1) {
-        c.sp = a.xpush[side] + xout * a.xpitch[side] + cb;
+        c.sp = gp(a.xpush[side]) + xout * a.xpitch[side] + cb;
         c.sps = sgn * a.xpitch[side];
       }
       if ((xpushes >> cn) & 1) {
-        c.cn = a.xpush[cn] + xout * a.xpitch[cn] + cb;
+        c.cn = gp(a.xpush[cn]) + xout * a.xpitch[cn] + cb;
         c.cns = sgn * a.xpitch[cn];
       }
       if ((xpushes >> cs) & 1) {
-        c.cs = a.xpush[cs] + xout * a.xpitch[cs] + cb;
+        c.cs = gp(a.xpush[cs]) + xout * a.xpitch[cs] + cb;
         c.css = sgn * a.xpitch[cs];
       }
     }
   }
 
   const int64_t soff = (a.G + xin) * a.pitch + a.PL + cb;
-  const float4* rowp = reinterpret_cast<const float4*>(a.src + soff);
-  const float4* hrowp = (ns_unit && a.hsrc[dir] != nullptr) ? reinterpret_cast<const float4*>(a.hsrc[dir] + soff)
+  const float4* rowp = reinterpret_cast<const float4*>(gp(a.src) + soff);
+  const float4* hrowp = (ns_unit && gp(a.hsrc[dir]) != nullptr) ? reinterpret_cast<const float4*>(gp(a.hsrc[dir]) + soff)
                                                             : rowp;
   // 2-D direct: lanes entirely left of column 0 / at or right of ycell are ghost columns — they
   // read every row (corners included) from my receive groups (the same pitch as the tile)
   if (xreads != 0) {
     const int64_t rb = (a.G + xin) * a.pitch;
     if (cb < 0 && (xreads & (kLinkW | kLinkNW | kLinkSW)) != 0) {
-      rowp = hrowp = reinterpret_cast<const float4*>(a.gsrc[0] + rb + kGhostGroup + cb);
+      rowp = hrowp = reinterpret_cast<const float4*>(gp(a.gsrc[0]) + rb + kGhostGroup + cb);
     } else if (cb >= a.ycell && (xreads & (kLinkE | kLinkNE | kLinkSE)) != 0) {
-      rowp = hrowp = reinterpret_cast<const float4*>(a.gsrc[1] + rb + min(cb - a.ycell, (int64_t)(kGhostGroup - 4)));
+      rowp = hrowp = reinterpret_cast<const float4*>(gp(a.gsrc[1]) + rb + min(cb - a.ycell, (int64_t)(kGhostGroup - 4)));
     }
   }
   const int64_t pitch4 = rev ? -(a.pitch >> 2) : (a.pitch >> 2);
@@ -724,7 +762,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
   Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
   double racc = 0.0;
   // signalling units: mid-unit signal point (or the end); others never signal
-  unsigned long long* sig = ns_unit ? a.sig[dir] : nullptr;
+  unsigned long long* sig = ns_unit ? gp(a.sig[dir]) : nullptr;
   const int sig_at = sig == nullptr ? -1
                      : ((u.flags & kUnitSigEnd) != 0 || a.sig_rows <= 0) ? (1 << 30)
                                                                           : 2 * K + ((a.sig_rows + 3) & ~3);
@@ -750,20 +788,23 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if (lane == 0)
       for (int i = 0; i < kSideLinks; ++i)
-        if ((xpushes >> i) & 1) __hip_atomic_fetch_add(a.xsig[i], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((xpushes >> i) & 1) __hip_atomic_fetch_add(gp(a.xsig[i]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if constexpr (RESID) {
     racc = wave_sum(racc);
     int slot = w + a.prot;
     if (slot >= a.nunits) slot -= a.nunits;
-    publish_partial(a.partials, slot, racc, a.nunits, a.dec, lane);
+    DecideArgs dec = a.dec;
+    dec.seq = seq;
+    publish_partial(gp(a.partials), slot, racc, a.nunits, dec, lane);
   }
-  if (replay_check && lid_old >= a.lid) report_timeout(a.timed_out, a.timed_out_host, kIntegReplay);
-  if (a.waves_done != nullptr) {
+  if (replay_check && (w == 0 ? lid_old >= lid : lid_old > lid))
+    report_timeout(gp(a.timed_out), gp(a.timed_out_host), kIntegReplay);
+  if (gp(a.waves_done) != nullptr) {
     // serial pipeline: this wave's stores are complete — the next exchange copy checks that every
     // wave of the launches before it got here
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(a.waves_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_fetch_add(gp(a.waves_done), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (stamping) {
     // the wave's stores have drained: its work is done, not just issued
@@ -771,7 +812,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     const unsigned hw = (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 16) | (__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xffffu);
     if (lane == 0) {
-      unsigned long long* s = a.stamps + 4 * (int64_t)w;
+      unsigned long long* s = gp(a.stamps) + 4 * (int64_t)w;
       s[0] = t_start;
       s[1] = t_ready;
       s[2] = t_end;
@@ -786,15 +827,19 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a) {
 // instantiated in its own generated translation unit (heat2d_amd/_build.py writes
 // build/gen/stream_k<K>_f<F32>r<RESID>.hip), so the 44 stencil objects compile in parallel.
 template <int K, bool F32, bool RESID>
-void launch_stream_kv(const StreamArgs& a, hipStream_t s) {
-  const int blocks = std::max(1, (a.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_kernels)
-  void (*fn)(StreamArgs) = a.wt ? stream_kernel<K, F32, RESID, true> : stream_kernel<K, F32, RESID, false>;
-  hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, a);
+void launch_stream_kv(const StreamArgs* blk, const StreamDyn& d, bool wt, hipStream_t s) {
+  const int blocks = std::max(1, (d.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_kernels)
+  StreamNeed need;
+  for (int i = 0; i < kNumDirs; ++i) need.v[i] = d.need[i];
+  void (*fn)(const StreamArgs*, unsigned long long, unsigned long long, unsigned long long, unsigned, StreamNeed) =
+      wt ? stream_kernel<K, F32, RESID, true> : stream_kernel<K, F32, RESID, false>;
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, blk, d.lid, d.copies_need, d.seq, d.btag, need);
 }
 
 template <int K, bool F32, bool RESID>
 int stream_blocks_per_cu_v() {
-  void (*fn)(StreamArgs) = stream_kernel<K, F32, RESID, false>;
+  void (*fn)(const StreamArgs*, unsigned long long, unsigned long long, unsigned long long, unsigned, StreamNeed) =
+      stream_kernel<K, F32, RESID, false>;
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), 256, 0) != hipSuccess) return 1;
   return nb > 0 ? nb : 1;

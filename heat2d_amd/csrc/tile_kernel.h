@@ -7,7 +7,9 @@ namespace h2d {
 
 // Arguments of the LDS-tiled temporally-blocked kernel (tile_kernel.hip): one NT-thread
 // workgroup per TX x TY tile, K steps per launch, region RY = TY + 2K columns (32, 64 or 128).
+// (the device-resident block: ArgBlocks, kernels.h)
 struct TileArgs {
+  ArgHead head;
   const float* src;  // owned cell (0, 0) of the single tile (whole grid)
   float* dst;
   int64_t pitch;
@@ -15,7 +17,7 @@ struct TileArgs {
   int TX, TY, RY, K;
   int NT = 256;  // threads per workgroup: 256 or 1024
   int CPL = 4;   // cells per lane and level: 1, 2 or 4 (RY / CPL <= 64: a region row in one wave)
-  int tiles_y = 0, ntiles = 0;  // set by launch_tile
+  int tiles_y = 0, ntiles = 0;  // set by prepare_tile
   double cx, cy;
   int fixed, per_x, per_y;
   double* partials;  // [ntiles] residual partials (residual launches)
@@ -25,7 +27,7 @@ struct TileArgs {
   // chunk; 0 = the last level K).  With rlev < K the launch goes on to level K, and a converged
   // check is rolled back by recomputation (keep must be null).
   int rlev = 0;
-  DecideArgs dec;         // residual launches: fused sum + decision (last block)
+  DecideArgs dec;         // residual launches: fused sum + decision (last block; seq: TileDyn::seq)
   // Deferred decision (fused check, lone tile): the PREVIOUS launch's check left `pend_n`
   // residual partials at `pend`; every block of this launch sums them in one fixed order before
   // its own work (the loads overlap its region loads) and does nothing if they converged, and
@@ -33,17 +35,27 @@ struct TileArgs {
   // partials: no drain, ticket or decision on its critical path.
   const double* pend = nullptr;
   int pend_n = 0;
-  DecideArgs pend_dec;
+  DecideArgs pend_dec;  // (seq: TileDyn::pend_seq)
+};
+// Per-launch part of a tiled launch.
+struct TileDyn {
+  unsigned long long seq = 0;       // check number of a deciding residual launch
+  unsigned long long pend_seq = 0;  // check number of the pending decision
+  unsigned btag = 0;                // the block's ArgHead::btag
 };
 size_t tile_lds_bytes(int TX, int RY, int K);
 // a lane owns up to kTileMaxSweeps region rows (kept in registers across the launch's levels)
 constexpr int kTileMaxSweeps = 8;
 bool tile_config_ok(int TX, int RY, int K, int CPL = 4, int NT = 256);
 int tile_count(int NX, int NY, int TX, int TY);
-void launch_tile(TileArgs a, int precision, bool residual, hipStream_t s);
+// Check a launch's configuration and fill tiles_y / ntiles (before the block is made).
+void prepare_tile(TileArgs& a);
+// `blk`: the device-resident copy of the prepared `host` arguments.
+void launch_tile(const TileArgs* blk, const TileArgs& host, const TileDyn& d, int precision, bool residual,
+                 hipStream_t s);
 // No-op launches of every tiled-kernel variant of `precision`: HIP loads a translation unit's
 // code object at its first launch (deferred loading, tens to hundreds of microseconds), which
 // must not land inside a timed run.
-void warm_tile_kernels(int precision, hipStream_t s);
+void warm_tile_kernels(int precision, hipStream_t s);  // (the zero block: no tiles)
 
 }  // namespace h2d

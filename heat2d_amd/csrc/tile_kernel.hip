@@ -88,7 +88,15 @@ __device__ __forceinline__ void group_update(const float (&N)[CPL], const float 
 }
 
 template <bool F32, bool RESID, int RY, int NT, int CPL>
-__global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
+__global__ __launch_bounds__(NT) void tile_lds_kernel(const TileArgs* __restrict__ ap, unsigned long long seq,
+                                                      unsigned long long pend_seq, unsigned btag) {
+  // (per-launch values read once, up front: see stream_kernel)
+  asm volatile("" : "+s"(seq), "+s"(pend_seq), "+s"(btag));
+  TileDyn d;
+  d.seq = seq;
+  d.pend_seq = pend_seq;
+  d.btag = btag;
+  const TileArgs& a = *ap;  // immutable device-resident block
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
   constexpr int G = RY / CPL;         // lanes per region row (a row stays inside one wave)
@@ -111,14 +119,17 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
   const int y0 = by * a.TY - K;  // global column of region column 0
   const bool live = (int)blockIdx.x < nt;  // ntiles == 0: a no-op launch (warm_tile_kernels)
   // unconditional load (a dummy zero word without a stop word): no branch, so no wait here
+  if (a.head.btag != d.btag) {  // a block the launch does not name: compute nothing (the host sees
+    return;                      // the unconverged decision record; never seen in practice)
+  }
   const unsigned long long stopped =
-      __hip_atomic_load(a.stop != nullptr ? a.stop : &g_tile_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_load(gp(a.stop) != nullptr ? gp(a.stop) : &g_tile_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the previous check's partials (deferred decision): wave 0 issues its loads before the region
   // loads; summed below in publish_partial's order (lane-strided, then the wave butterfly)
   double pend_s = 0.0;
-  const bool pend = live && a.pend != nullptr;
+  const bool pend = live && gp(a.pend) != nullptr;
   if (pend && tid < 64)
-    for (int i = tid; i < a.pend_n; i += 64) pend_s += a.pend[i];
+    for (int i = tid; i < a.pend_n; i += 64) pend_s += gp(a.pend)[i];
   float* cur = lds;
   float* nxt = lds + RX * W;
 
@@ -140,7 +151,7 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
         else in = gr >= 0 && gr < a.NX;
         if (a.per_y) gc = wrap_idx(gc, a.NY);
         else in = in && gc >= 0 && gc < a.NY;
-        if (in) v[u] = a.src[(int64_t)gr * a.pitch + gc];
+        if (in) v[u] = gp(a.src)[(int64_t)gr * a.pitch + gc];
       }
     }
 #pragma unroll
@@ -158,8 +169,10 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
       const bool conv = tot < a.pend_dec.sens;
       pend_stop = (stopped != 0ull || conv) ? 1 : 0;
       if (blockIdx.x == 0 && stopped == 0ull) {
-        *a.pend_dec.total = tot;
-        decide_total(tot, a.pend_dec);  // the stop word for later launches, the host record
+        DecideArgs pd = a.pend_dec;
+        pd.seq = d.pend_seq;
+        *gp(pd.total) = tot;
+        decide_total(tot, pd);  // the stop word for later launches, the host record
       }
     }
   }
@@ -265,39 +278,50 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(TileArgs a) {
       double tot = part[0];
 #pragma unroll
       for (int w = 1; w < NW; ++w) tot += part[w];
-      publish_partial(a.partials, blockIdx.x, tot, a.ntiles, a.dec, tid);
+      DecideArgs dec = a.dec;
+      dec.seq = d.seq;
+      publish_partial(gp(a.partials), blockIdx.x, tot, a.ntiles, dec, tid);
     }
   }
   const int xs = bx * a.TX, ys = by * a.TY;
   for (int e = tid; e < a.TX * a.TY; e += NT) {
     const int i = e / a.TY, j = e - i * a.TY;
     if (xs + i < a.NX && ys + j < a.NY) {
-      a.dst[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + K + j];
+      gp(a.dst)[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + K + j];
       // after the final swap `nxt` holds level K-1
-      if (RESID && a.keep != nullptr) a.keep[(int64_t)(xs + i) * a.pitch + (ys + j)] = nxt[(K + i) * W + K + j];
+      if (RESID && gp(a.keep) != nullptr) gp(a.keep)[(int64_t)(xs + i) * a.pitch + (ys + j)] = nxt[(K + i) * W + K + j];
     }
   }
 }
 
+// host: the launch's configuration (template dispatch, grid); blk / d: the kernel's arguments
+struct TileLaunch {
+  const TileArgs* blk;
+  const TileArgs& host;
+  const TileDyn& d;
+};
+
 template <bool F32, bool RESID, int NT, int CPL>
-void launch_cpl(const TileArgs& a, size_t lds, hipStream_t s) {
+void launch_cpl(const TileLaunch& L, size_t lds, hipStream_t s) {
+  const TileArgs& a = L.host;
   const dim3 grid((unsigned)std::max(1, a.ntiles)), block(NT);  // ntiles == 0: no-op launch (warm_kernels)
-  if (a.RY == 32) hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 32, NT, CPL>), grid, block, lds, s, a);
-  else if (a.RY == 64) hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 64, NT, CPL>), grid, block, lds, s, a);
-  else if constexpr (CPL >= 2) hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 128, NT, CPL>), grid, block, lds, s, a);
+  if (a.RY == 32) hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 32, NT, CPL>), grid, block, lds, s, L.blk, L.d.seq, L.d.pend_seq, L.d.btag);
+  else if (a.RY == 64) hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 64, NT, CPL>), grid, block, lds, s, L.blk, L.d.seq, L.d.pend_seq, L.d.btag);
+  else if constexpr (CPL >= 2)
+    hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 128, NT, CPL>), grid, block, lds, s, L.blk, L.d.seq, L.d.pend_seq, L.d.btag);
 }
 
 template <bool F32, bool RESID, int NT>
-void launch_nt(const TileArgs& a, size_t lds, hipStream_t s) {
-  if (a.CPL == 1) launch_cpl<F32, RESID, NT, 1>(a, lds, s);
-  else if (a.CPL == 2) launch_cpl<F32, RESID, NT, 2>(a, lds, s);
-  else launch_cpl<F32, RESID, NT, 4>(a, lds, s);
+void launch_nt(const TileLaunch& L, size_t lds, hipStream_t s) {
+  if (L.host.CPL == 1) launch_cpl<F32, RESID, NT, 1>(L, lds, s);
+  else if (L.host.CPL == 2) launch_cpl<F32, RESID, NT, 2>(L, lds, s);
+  else launch_cpl<F32, RESID, NT, 4>(L, lds, s);
 }
 
 template <bool F32, bool RESID>
-void launch_ry(const TileArgs& a, size_t lds, hipStream_t s) {
-  if (a.NT == 1024) launch_nt<F32, RESID, 1024>(a, lds, s);
-  else launch_nt<F32, RESID, 256>(a, lds, s);
+void launch_ry(const TileLaunch& L, size_t lds, hipStream_t s) {
+  if (L.host.NT == 1024) launch_nt<F32, RESID, 1024>(L, lds, s);
+  else launch_nt<F32, RESID, 256>(L, lds, s);
 }
 
 }  // namespace
@@ -310,7 +334,7 @@ bool tile_config_ok(int TX, int RY, int K, int CPL, int NT) {
   return (RY == 32 || RY == 64 || RY == 128) && K >= 1 && RY - 2 * K >= 4 && TX >= 1 && tile_lds_bytes(TX, RY, K) <= 65536;
 }
 
-void launch_tile(TileArgs a, int precision, bool residual, hipStream_t s) {
+void prepare_tile(TileArgs& a) {
   if (!tile_config_ok(a.TX, a.RY, a.K, a.CPL, a.NT)) throw std::invalid_argument("launch_tile: bad tile configuration");
   if (a.TY != a.RY - 2 * a.K) throw std::invalid_argument("launch_tile: TY must be RY - 2K");
   if (a.rlev < 0 || a.rlev > a.K || (a.rlev != 0 && a.rlev != a.K && a.keep != nullptr))
@@ -318,34 +342,46 @@ void launch_tile(TileArgs a, int precision, bool residual, hipStream_t s) {
   if (a.NT != 256 && a.NT != 1024) throw std::invalid_argument("launch_tile: NT must be 256 or 1024");
   a.tiles_y = (a.NY + a.TY - 1) / a.TY;
   a.ntiles = ((a.NX + a.TX - 1) / a.TX) * a.tiles_y;
+}
+
+void launch_tile(const TileArgs* blk, const TileArgs& a, const TileDyn& d, int precision, bool residual,
+                 hipStream_t s) {
+  if (blk == nullptr || d.btag != a.head.btag || a.ntiles != ((a.NX + a.TX - 1) / a.TX) * a.tiles_y)
+    throw std::invalid_argument("launch_tile: the launch does not name its prepared argument block");
   const size_t lds = tile_lds_bytes(a.TX, a.RY, a.K);
   const bool f32 = precision == kFp32;
+  const TileLaunch L{blk, a, d};
   if (f32) {
-    if (residual) launch_ry<true, true>(a, lds, s);
-    else launch_ry<true, false>(a, lds, s);
+    if (residual) launch_ry<true, true>(L, lds, s);
+    else launch_ry<true, false>(L, lds, s);
   } else {
-    if (residual) launch_ry<false, true>(a, lds, s);
-    else launch_ry<false, false>(a, lds, s);
+    if (residual) launch_ry<false, true>(L, lds, s);
+    else launch_ry<false, false>(L, lds, s);
   }
   H2D_HIP_CHECK(hipGetLastError());
 }
 
 void warm_tile_kernels(int precision, hipStream_t s) {
+  static_assert(sizeof(TileArgs) <= kZeroArgBytes, "the zero block covers the tiled arguments");
+  // the zero block: no tiles (every workgroup exits after its empty region load)
+  const TileArgs* z = static_cast<const TileArgs*>(zero_arg_block());
   TileArgs a{};
   a.ntiles = 0;
   a.tiles_y = 1;
+  const TileDyn d;
   const bool f32 = precision == kFp32;
   for (int ry : {32, 64, 128})
     for (int nt : {256, 1024})
       for (int cpl : {1, 2, 4}) {
         if (!tile_config_ok(1, ry, 1, cpl, nt)) continue;
         a.RY = ry, a.NT = nt, a.CPL = cpl;
+        const TileLaunch L{z, a, d};
         if (f32) {
-          launch_ry<true, true>(a, 0, s);
-          launch_ry<true, false>(a, 0, s);
+          launch_ry<true, true>(L, 0, s);
+          launch_ry<true, false>(L, 0, s);
         } else {
-          launch_ry<false, true>(a, 0, s);
-          launch_ry<false, false>(a, 0, s);
+          launch_ry<false, true>(L, 0, s);
+          launch_ry<false, false>(L, 0, s);
         }
       }
   H2D_HIP_CHECK(hipGetLastError());

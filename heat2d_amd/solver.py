@@ -16,10 +16,8 @@ Execution modes
 """
 from __future__ import annotations
 
-import os
 import socket
 import time
-import warnings
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -119,11 +117,6 @@ class Solver:
                 ranks = [0]
         elif world == 1:
             transport = n.TRANSPORT_LOCAL
-            if self.on_gpu and len(ranks) > 1 and os.environ.get("HIP_FORCE_DEV_KERNARG") == "1":
-                # several tiles in one process is the pattern that read stale kernel arguments
-                # from the device-memory pool (docs/ARCHITECTURE.md, "Stale kernel arguments")
-                warnings.warn("local multi-tile GPU run with HIP_FORCE_DEV_KERNARG=1: launches may read stale kernel "
-                              "arguments; unset it (heat2d_amd defaults to 0) for a safe run", RuntimeWarning)
         elif self.on_gpu and cfg.transport in ("auto", "rccl"):
             transport = n.TRANSPORT_RCCL
         else:

@@ -213,17 +213,23 @@ def test_host_sanitizers_engine_cpu_path(native, tmp_path):
 
 def test_kernel_arguments_default_to_host_memory():
     """Importing heat2d_amd selects host-memory kernel arguments for the HIP runtime unless the
-    user chose (docs/ARCHITECTURE.md, "Stale kernel arguments"); a fresh interpreter, so the
-    setting is seen before anything initialises the GPU."""
+    user chose (docs/ARCHITECTURE.md, "Kernel arguments and metadata memory"), and records the
+    effective state; the CLI does the same, and bench.py runs the library default (no override of
+    its own), so the bench times what the tests run.  A fresh interpreter, so the setting is seen
+    before anything initialises the GPU."""
     import subprocess
     import sys
 
-    code = "import os, heat2d_amd; print(os.environ['HIP_FORCE_DEV_KERNARG'])"
+    code = "import os, heat2d_amd; print(os.environ['HIP_FORCE_DEV_KERNARG'], heat2d_amd.KERNARG_HOST_MEMORY)"
     env = {k: v for k, v in os.environ.items() if k != "HIP_FORCE_DEV_KERNARG"}
     env["HEAT2D_NO_BUILD"] = "1"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
-    assert out.stdout.split()[-1] == "0"
+    assert out.stdout.split()[-2:] == ["0", "True"]
     env["HIP_FORCE_DEV_KERNARG"] = "1"  # the user's choice is kept
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
-    assert out.stdout.split()[-1] == "1"
+    assert out.stdout.split()[-2:] == ["1", "False"]
+    with open(os.path.join(root, "bench.py")) as fh:
+        assert "HIP_FORCE_DEV_KERNARG" not in fh.read()
+    with open(os.path.join(root, "heat2d_amd", "csrc", "heat2d_main.cpp")) as fh:
+        assert 'setenv("HIP_FORCE_DEV_KERNARG", "0", 0)' in fh.read()

@@ -508,9 +508,10 @@ def _outside_nonzero(eng, t, b):
 # Engine orders: the previous engine released before the next is built (release-first), the
 # next built while the previous is alive and the previous released right before the run
 # (create-first: the plain `eng = Engine(...)` in a loop), and the previous kept alive through the
-# run (create-keep).  With the HIP runtime's kernel arguments in device memory, the create-* orders
-# computed wrong tiles in the long GPU test process and once faulted (stale kernel arguments:
-# docs/ARCHITECTURE.md); heat2d_amd keeps them in host memory by default, which this test checks.
+# run (create-keep).  With the HIP runtime's kernel arguments in device memory these orders
+# computed wrong tiles in the long GPU test process and sometimes faulted (rounds 3-5); the
+# library's default (host-memory arguments, free since round 5's preloaded kernel arguments) is
+# what this test runs (docs/ARCHITECTURE.md, "Kernel arguments and metadata memory").
 _SERIAL_ORDERS = ["release-first", "create-first", "create-keep"] + [o for o in os.environ.get("H2D_SERIAL_ORDERS", "").split(",") if o]
 
 
@@ -530,9 +531,16 @@ def test_serial_tiles_long_convergence_run(native, gpu, gx, gy, order):
             eng = None  # the previous engine is released before the next one is built
         elif order == "create-keep":
             kept.append(eng)  # the previous engine stays alive through the next run
+        # canary (create-keep): every byte of the kept engines' storage, before the next run
+        canary = [(k, t, b, k.storage(t, b)) for k in kept if k is not None for t in range(k.num_tiles())
+                  for b in (0, 1)]
         eng = native.Engine(nx, ny, gridx=gx, gridy=gy, boundary=1, tblock=8, device=gpu, fused_check=fused,
                             small_grid_lds=False, tiled=0, overlap=False, **CONV)
         st = eng.run(3000)
+        for k, t, b, before in canary:  # an idle engine's memory: no stray writer touched it
+            after = k.storage(t, b)
+            assert np.array_equal(before.view(np.uint32), after.view(np.uint32)), \
+                f"kept engine tile {t} buffer {b}: {int((before.view(np.uint32) != after.view(np.uint32)).sum())} words changed"
         got = _gather(eng, nx, ny)
         if not (st["converged"] and st["steps_done"] == ref["steps_done"] and np.array_equal(got, ref["grid"])):
             want = oracle(native, nx, ny, int(st["steps_done"]), 1)["grid"]
