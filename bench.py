@@ -317,6 +317,13 @@ def main() -> int:
     plaunches = ctx.gather_objects(int(s.engine.pstream_launches()))
 
     # ---- in-job single-GPU reference: speedup / efficiency, and bit-exact verification ------
+    # (the timed solver is closed first: no two engines coexist on a rank's GPU in the bench)
+    digests = None
+    if world > 1 and not a.no_reference and not fill_hbm and scaling == "strong":
+        digests = ctx.gather_objects(B.grid_digest(s.tiles()))
+    holder.pop("solver").close()
+    del s
+    ctx.barrier()
     t1 = None
     verified_full = None
     ref_note = None
@@ -328,7 +335,6 @@ def main() -> int:
     elif not a.no_reference and not fill_hbm:
         # strong: the same global grid on rank 0's GPU alone; weak: one GPU's tile alone
         rnx, rny = (nx, ny) if scaling == "strong" else (side, side)
-        digests = ctx.gather_objects(B.grid_digest(s.tiles()) if scaling == "strong" else None)
         if ctx.rank == 0:
             e = n.Engine(rnx, rny, boundary=bnd, precision=prec, tblock=ref_tblock, rows_per_wave=a.rows_per_wave,
                          device=device, small_grid_lds=False)

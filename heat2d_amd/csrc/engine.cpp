@@ -386,6 +386,13 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
           T.pcap = need;
           T.partials = dmalloc<double>((size_t)need);
         }
+        if (recompute_rollback() && T.spare == nullptr) {
+          // the third buffer of the speculative launches after checks (run_tiled): a copy of
+          // the second (its ghost ring / poison included; the kernel writes only in-grid cells)
+          const size_t n = (size_t)T.g.elems();
+          T.spare = dmalloc<float>(n);
+          H2D_HIP_CHECK(hipMemcpyAsync(T.spare, T.buf[1], n * sizeof(float), hipMemcpyDeviceToDevice, compute_));
+        }
       }
     }
     if (!opt_.naive) warm_stream_kernels(opt_.precision, G_, compute_);
@@ -408,6 +415,7 @@ Engine::~Engine() {
   for (auto& t : tiles_) {
     for (int b = 0; b < 2; ++b) hipFree(t.buf[b]);
     if (t.keep) hipFree(t.keep);
+    if (t.spare) hipFree(t.spare);
   }
   if (h_conv_) hipHostFree(h_conv_);
   if (ev_check_) hipEventDestroy(ev_check_);
@@ -1303,8 +1311,11 @@ void Engine::run_tiled(RunStats& st, int64_t target) {
     TileArgs a;
     zero_args(a);
     TileDyn dy;
+    // the launch after a check decides it in its extra block while its tiles compute: it must
+    // not write the check's input (the rollback recomputes from it), so it writes the spare
+    const bool to_spare = span && pend && T.spare != nullptr;
     a.src = T.buf[T.cur] + T.g.idx(0, 0);
-    a.dst = T.buf[1 - T.cur] + T.g.idx(0, 0);
+    a.dst = (to_spare ? T.spare : T.buf[1 - T.cur]) + T.g.idx(0, 0);
     a.pitch = T.g.pitch;
     a.NX = (int)T.g.xcell;
     a.NY = (int)T.g.ycell;
@@ -1354,6 +1365,7 @@ void Engine::run_tiled(RunStats& st, int64_t target) {
     launch_tile(blk, a, dy, opt_.precision, check, compute_);
     trace_end("step", compute_);
     if (check && !fused_) launch_reduce_sum(a.partials, tile_count(a.NX, a.NY, a.TX, a.TY), d_resid_, compute_);
+    if (to_spare) std::swap(T.spare, T.buf[1 - T.cur]);  // the check's input becomes the spare
     T.cur = 1 - T.cur;
     ++st.chunks;
     if (check) {
@@ -1787,7 +1799,8 @@ bool Engine::check_point(int64_t steps_before, int k, int lvl) {
   // launches queued after the converged one are no-ops on the device).
   const unsigned long long seq = ++chunk_seq_;
   // cur has flipped past the chunk; lvl: the check's level in the chunk (k: its last)
-  checks_.push_back(CheckRec{seq, steps_before, k, 1 - tiles_[0].cur, lvl > 0 ? lvl : k});
+  checks_.push_back(CheckRec{seq, steps_before, k, 1 - tiles_[0].cur, tiles_[0].buf[1 - tiles_[0].cur],
+                            lvl > 0 ? lvl : k});
   if (!decided_in_launch_) device_decide(seq);
   decided_in_launch_ = false;
   if (rccl_comm_) {
@@ -1814,9 +1827,16 @@ bool Engine::finalize_convergence(RunStats& st) {
     st.residual = h_conv_->residual;
     H2D_HIP_CHECK(hipMemsetAsync(d_stop_, 0, sizeof(unsigned long long), compute_));
     if (recompute_rollback()) {
-      // the launches after the converged check were no-ops, so the check chunk's input buffer
-      // still holds the state at steps_before: advance it k-1 steps (plain launches, no check)
-      tiles_[0].cur = it->src;
+      // the launches after the converged check were no-ops (or, tiled, wrote the spare buffer),
+      // so the check chunk's input buffer still holds the state at steps_before: advance it
+      // lvl-1 steps (plain launches, no check)
+      Tile& T0 = tiles_[0];
+      if (T0.buf[it->src] != it->src_ptr) {  // moved by the tiled path's rotation: bring it back
+        float** at = T0.buf[1 - it->src] == it->src_ptr ? &T0.buf[1 - it->src] : &T0.spare;
+        if (*at != it->src_ptr) throw std::logic_error("converged check's input buffer not found");
+        std::swap(*at, T0.buf[it->src]);
+      }
+      T0.cur = it->src;
       launched = it->lvl > 1;
       for (int left = it->lvl - 1; left > 0;) {
         int kk = std::min(left, G_);

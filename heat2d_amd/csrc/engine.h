@@ -258,6 +258,9 @@ class Engine {
     TileGeom g;
     float* buf[2] = {nullptr, nullptr};  // device or host storage
     float* keep = nullptr;               // fused convergence: state one step before the last check
+    // tiled lone tile with the fused check: the third buffer of the speculative launch after a
+    // check (TileArgs::pend): that launch writes here, so the check's input survives it
+    float* spare = nullptr;
     std::vector<float> host[2];          // CPU storage
     std::vector<float> scratch[2];       // CPU temporal-block scratch
     int cur = 0;
@@ -448,6 +451,7 @@ class Engine {
     int64_t steps_before;
     int k;
     int src;  // the check chunk's input buffer (tile 0): unchanged by the no-op launches after it
+    const float* src_ptr;  // its storage (the tiled path's three-buffer rotation moves it)
     int lvl;  // the check step's level in the chunk (== k unless the chunk runs through the check)
   };
   // A lone single-process tile keeps no rollback copy in its check launches: on convergence

@@ -29,10 +29,13 @@ struct TileArgs {
   int rlev = 0;
   DecideArgs dec;         // residual launches: fused sum + decision (last block; seq: TileDyn::seq)
   // Deferred decision (fused check, lone tile): the PREVIOUS launch's check left `pend_n`
-  // residual partials at `pend`; every block of this launch sums them in one fixed order before
-  // its own work (the loads overlap its region loads) and does nothing if they converged, and
-  // block 0 records the decision (pend_dec).  The check launch itself then only stores its
-  // partials: no drain, ticket or decision on its critical path.
+  // residual partials at `pend`; one extra block of this launch (blockIdx ntiles) sums them in
+  // one fixed order and records the decision (pend_dec) while the tile blocks compute this
+  // launch SPECULATIVELY: a converged check makes the launches after this one no-ops (they read
+  // the stop word), and this one writes a buffer that is not the check's input (the engine
+  // rotates three buffers in this mode), so the rollback's recompute still finds that input.
+  // The check launch itself only stores its partials: no drain, ticket or decision on the
+  // critical path of either launch.
   const double* pend = nullptr;
   int pend_n = 0;
   DecideArgs pend_dec;  // (seq: TileDyn::pend_seq)

@@ -56,6 +56,46 @@ __device__ __forceinline__ void lds_put(float* p, const float (&v)[CPL]) {
   else *p = v[0];
 }
 
+// Sum over the wave, every lane gets it: DPP within each 16-lane row (quad swaps, then row
+// rotations by 4 and 8: no LDS traffic, unlike the ds_bpermute butterfly), then the four row
+// sums read from lanes 0 / 16 / 32 / 48 and added in that order.  fp64 moves as two 32-bit halves.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double lane_f64(double v, int lane) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)b, lane);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double dpp_wave_sum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x124>(v);  // row_ror:4
+  v += dpp_f64<0x128>(v);  // row_ror:8
+  return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
+}
+
+// The deferred decision of the previous launch's check (one wave of the deciding block): the
+// partials summed lane-strided, then over the wave; the stop word and the host record.
+__device__ __forceinline__ void decide_pending(const TileArgs& a, unsigned long long pend_seq, int lane) {
+  const unsigned long long* stop = gp(a.pend_dec.stop);
+  if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;  // decided earlier
+  double s = 0.0;
+  for (int i = lane; i < a.pend_n; i += 64) s += gp(a.pend)[i];
+  s = dpp_wave_sum(s);
+  if (lane == 0) {
+    DecideArgs pd = a.pend_dec;
+    pd.seq = pend_seq;
+    *gp(pd.total) = s;
+    decide_total(s, pd);  // the stop word for later launches, the host record
+  }
+}
+
 // One time level of a lane's CPL cells from rows r-1 (N), r (C), r+1 (S).  The west / east
 // neighbours of the group are the adjacent lanes' last / first cell (DPP wave shifts: a region
 // row is RY/CPL consecutive lanes of one wave); the first / last lane of a row reads another
@@ -118,25 +158,25 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(const TileArgs* __restrict
   const int x0 = bx * a.TX - K;  // global row of region row 0
   const int y0 = by * a.TY - K;  // global column of region column 0
   const bool live = (int)blockIdx.x < nt;  // ntiles == 0: a no-op launch (warm_tile_kernels)
-  // unconditional load (a dummy zero word without a stop word): no branch, so no wait here
   if (a.head.btag != d.btag) {  // a block the launch does not name: compute nothing (the host sees
     return;                      // the unconverged decision record; never seen in practice)
   }
+  if (!live) {
+    // the deciding block (grid = ntiles + 1 when `pend`): the previous check's decision, off the
+    // tile blocks' critical path (they compute speculatively, see TileArgs::pend)
+    if ((int)blockIdx.x == nt && nt > 0 && gp(a.pend) != nullptr && tid < 64) decide_pending(a, d.pend_seq, tid);
+    return;
+  }
+  // unconditional load (a dummy zero word without a stop word): no branch, so no wait here
   const unsigned long long stopped =
       __hip_atomic_load(gp(a.stop) != nullptr ? gp(a.stop) : &g_tile_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the previous check's partials (deferred decision): wave 0 issues its loads before the region
-  // loads; summed below in publish_partial's order (lane-strided, then the wave butterfly)
-  double pend_s = 0.0;
-  const bool pend = live && gp(a.pend) != nullptr;
-  if (pend && tid < 64)
-    for (int i = tid; i < a.pend_n; i += 64) pend_s += gp(a.pend)[i];
   float* cur = lds;
   float* nxt = lds + RX * W;
 
   // ---- load the region (zero outside a non-periodic grid); LB loads in flight per thread
   // before the LDS stores wait on them (one global round trip per LB·NT cells, not per NT) ----
   constexpr int LB = 4;
-  const int total = live ? RX * RY : 0;
+  const int total = RX * RY;
   for (int e0 = tid; e0 < total; e0 += LB * NT) {
     float v[LB];
 #pragma unroll
@@ -158,24 +198,9 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(const TileArgs* __restrict
     for (int u = 0; u < LB; ++u)
       if (e0 + u * NT < total) cur[e0 + u * NT] = v[u];  // W == RY: region element e lives at cur[e]
   }
-  if (!live) return;
-  if (!pend && stopped != 0ull) return;  // converged earlier (the word is stable in launches without `pend`)
-  // `pend`: block 0 sets the stop word DURING this launch, so the decision to do nothing is made
-  // once per workgroup (thread 0), shared through LDS and read after the barrier below
-  __shared__ int pend_stop;
-  if (pend && tid < 64) {
-    const double tot = wave_sum(pend_s);
-    if (tid == 0) {
-      const bool conv = tot < a.pend_dec.sens;
-      pend_stop = (stopped != 0ull || conv) ? 1 : 0;
-      if (blockIdx.x == 0 && stopped == 0ull) {
-        DecideArgs pd = a.pend_dec;
-        pd.seq = d.pend_seq;
-        *gp(pd.total) = tot;
-        decide_total(tot, pd);  // the stop word for later launches, the host record
-      }
-    }
-  }
+  // converged earlier (set by an earlier launch's deciding block, or during this launch by its
+  // own: then this launch's output is discarded anyway)
+  if (stopped != 0ull) return;
 
   // ---- per-thread column group and its edge masks (fixed: hold, ghost-zero: zero) ----
   const int q = tid % G;
@@ -201,7 +226,6 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(const TileArgs* __restrict
   const Coef k{a.cx, a.cy, (float)a.cx, (float)a.cy};
   double racc = 0.0;
   __syncthreads();
-  if (pend && pend_stop != 0) return;  // converged: this launch is a no-op (uniform per workgroup)
 
   // ---- this lane's rows r_j = r_off + j·RSTEP (j < MJ) stay fixed for the whole launch: their
   // cells live in registers across levels (only rows r±1 are read from LDS), and their edge
@@ -266,12 +290,21 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(const TileArgs* __restrict
     for (int t = rlev + 1; t <= K; ++t) level(t, std::false_type{});
   }
 
-  // ---- the residual partial first (its store and, with a ticket, the decision overlap the
-  // write-back below), then the owned tile ----
+  // ---- the owned tile, then the residual partial (its reduction overlaps the write-back's
+  // stores; with a ticket the last block also decides) ----
+  const int xs = bx * a.TX, ys = by * a.TY;
+  for (int e = tid; e < a.TX * a.TY; e += NT) {
+    const int i = e / a.TY, j = e - i * a.TY;
+    if (xs + i < a.NX && ys + j < a.NY) {
+      gp(a.dst)[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + K + j];
+      // after the final swap `nxt` holds level K-1
+      if (RESID && gp(a.keep) != nullptr) gp(a.keep)[(int64_t)(xs + i) * a.pitch + (ys + j)] = nxt[(K + i) * W + K + j];
+    }
+  }
   if constexpr (RESID) {
     constexpr int NW = NT / 64;
     __shared__ double part[NW];
-    racc = wave_sum(racc);
+    racc = dpp_wave_sum(racc);
     if ((tid & 63) == 0) part[tid >> 6] = racc;
     __syncthreads();
     if (tid < 64) {
@@ -281,15 +314,6 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(const TileArgs* __restrict
       DecideArgs dec = a.dec;
       dec.seq = d.seq;
       publish_partial(gp(a.partials), blockIdx.x, tot, a.ntiles, dec, tid);
-    }
-  }
-  const int xs = bx * a.TX, ys = by * a.TY;
-  for (int e = tid; e < a.TX * a.TY; e += NT) {
-    const int i = e / a.TY, j = e - i * a.TY;
-    if (xs + i < a.NX && ys + j < a.NY) {
-      gp(a.dst)[(int64_t)(xs + i) * a.pitch + (ys + j)] = cur[(K + i) * W + K + j];
-      // after the final swap `nxt` holds level K-1
-      if (RESID && gp(a.keep) != nullptr) gp(a.keep)[(int64_t)(xs + i) * a.pitch + (ys + j)] = nxt[(K + i) * W + K + j];
     }
   }
 }
@@ -304,7 +328,8 @@ struct TileLaunch {
 template <bool F32, bool RESID, int NT, int CPL>
 void launch_cpl(const TileLaunch& L, size_t lds, hipStream_t s) {
   const TileArgs& a = L.host;
-  const dim3 grid((unsigned)std::max(1, a.ntiles)), block(NT);  // ntiles == 0: no-op launch (warm_kernels)
+  // ntiles == 0: no-op launch (warm_kernels); a pending decision: one more (deciding) block
+  const dim3 grid((unsigned)std::max(1, a.ntiles + (a.pend != nullptr && a.ntiles > 0 ? 1 : 0))), block(NT);
   if (a.RY == 32) hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 32, NT, CPL>), grid, block, lds, s, L.blk, L.d.seq, L.d.pend_seq, L.d.btag);
   else if (a.RY == 64) hipLaunchKernelGGL((tile_lds_kernel<F32, RESID, 64, NT, CPL>), grid, block, lds, s, L.blk, L.d.seq, L.d.pend_seq, L.d.btag);
   else if constexpr (CPL >= 2)
