@@ -395,6 +395,18 @@ Engine::Engine(const EngineOptions& o) : opt_(o) {
         }
       }
     }
+    if (recompute_rollback() && !tiled_ && !opt_.naive && tiles_[0].spare == nullptr) {
+      // a lone streaming tile's third buffer (speculative launch after a check, StreamArgs::pend)
+      // where it costs at most an eighth of the free memory (not for HBM-filling tiles: those
+      // keep the separate decision kernel)
+      const size_t n = (size_t)tiles_[0].g.elems();
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) == hipSuccess && n * sizeof(float) <= fr / 8) {
+        tiles_[0].spare = dmalloc<float>(n);
+        H2D_HIP_CHECK(hipMemcpyAsync(tiles_[0].spare, tiles_[0].buf[1], n * sizeof(float), hipMemcpyDeviceToDevice,
+                                     compute_));
+      }
+    }
     if (!opt_.naive) warm_stream_kernels(opt_.precision, G_, compute_);
     if (!opt_.naive && (opt_.persistent > 0 || (opt_.persistent < 0 && direct_)))
       warm_pstream_kernels(opt_.precision, G_, compute_);
@@ -658,10 +670,12 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     L.d_bfirst = dmalloc<Unit>(bfirst.size());
     h2d(L.d_bfirst, bfirst.data(), bfirst.size() * sizeof(Unit));
     Tile& tw = tiles_[t];
-    if ((int64_t)all.size() > tw.pcap) {
+    // two sets: a lone tile's check partials are read by the next launch's deciding block while
+    // that launch may store its own check's
+    if (2 * (int64_t)all.size() > tw.pcap) {
       H2D_HIP_CHECK(hipDeviceSynchronize());
       hipFree(tw.partials);
-      tw.pcap = std::max<int64_t>((int64_t)all.size(), 256);
+      tw.pcap = std::max<int64_t>(2 * (int64_t)all.size(), 256);
       tw.partials = dmalloc<double>((size_t)tw.pcap);
     }
   }
@@ -706,6 +720,22 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   // launch (device_decide).  (A last-wave in-kernel reduction was measured slower here: 1024
   // waves' ticket atomics on one address serialise; the tiled kernel, with few blocks, uses it.)
   const bool lone = fused_ && tiles_.size() == 1 && !rccl_comm_ && !direct_;
+  // lone tile with a spare buffer: its check partials alternate between two sets, and the launch
+  // after a check decides it in an extra block while its units compute into the spare buffer
+  // (the check's input must survive: a converged check is rolled back by recomputing from it)
+  const bool spec = lone && which == 0 && src == tl.cur && tl.spare != nullptr && stream == nullptr;
+  if (spec && residual) a.partials = tl.partials + (size_t)pset_ * (size_t)(tl.pcap / 2);
+  bool to_spare = false;
+  if (spec && pend_parts_ != nullptr) {
+    a.pend = pend_parts_;
+    a.pend_n = pend_nparts_;
+    a.pend_dec = pend_dec_;
+    a.pend_dec.seq = 0;  // (per launch: StreamDyn::seq)
+    dy.seq = pend_dec_.seq;
+    a.dst = tl.spare;
+    to_spare = true;
+    pend_parts_ = nullptr;
+  }
   if (fused_) {
     a.stop = d_stop_;
     // the rollback copy: a lone tile recomputes it on convergence instead (no 4 B/cell write per check)
@@ -809,13 +839,16 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   const StreamArgs* blk = args_.get(a, ls);  // the plan-constant part: device-resident, uploaded once
   dy.nunits = a.nunits;
   dy.btag = a.head.btag;
+  dy.pend = a.pend != nullptr;
   launch_stream(blk, a, dy, K, opt_.precision, residual, ls);
+  if (to_spare) std::swap(tl.spare, tl.buf[1 - src]);  // the check's input becomes the spare
   if (a.waves_done != nullptr) waves_need_ += (unsigned long long)a.nunits;
   progress_tick(ls);
   if (residual && whole && !lone) reduce_tile_residual(t, K);
   if (residual && whole && lone) {
-    last_parts_ = tl.partials;
+    last_parts_ = a.partials;
     last_nparts_ = L.n_all;
+    if (spec) pset_ ^= 1;
   }
 }
 
@@ -1244,6 +1277,7 @@ RunStats Engine::run_impl(int64_t steps) {
     else if (has_exchange_ && sig_mode_ > 0) run_signal(st, target);
     else run_serial(st, target);
   }
+  flush_pending_decision();  // the run's last check, not followed by a launch
   end_of_run_wait(st, w0);
   poll_abort();
   if (fused_ && finalize_convergence(st)) end_of_run_wait(st, w0);  // times include the recompute launches
@@ -1545,6 +1579,7 @@ void Engine::run_serial(RunStats& st, int64_t target) {
       // a run of equal plain chunks: ONE persistent launch
       const int J = plain_run(steps_done_, target, k);
       if (J >= 2 && pplan(k) != nullptr) {
+        flush_pending_decision();  // (a persistent launch carries no deciding block)
         trace_begin("step", compute_);
         launch_pstream_chunks(k, J);
         trace_end("step", compute_);
@@ -1615,7 +1650,7 @@ const Engine::PPlan* Engine::pplan(int K) {
                     (opt_.persistent < 0 && direct_ && has_exchange_ && g.xcell <= 1536 && opt_.timeline == 0 && K >= 2);
   // (every wave must be resident: not with CUs reserved for the comm stream)
   const bool ok_path = on_gpu() && !opt_.naive && !tiled_ && want && tiles_.size() == 1 && K <= kMaxPK && K <= G_ &&
-                       stream_k_supported(K) && !fused_ && comm_cus_ == 0;
+                       stream_k_supported(K) && comm_cus_ == 0;
   bool halo_n = false, halo_s = false, ok = ok_path;
   if (ok && has_exchange_) {
     // only the direct pipeline of 1-D row strips (no west / east / corner neighbours)
@@ -1694,6 +1729,7 @@ void Engine::launch_pstream_chunks(int K, int J) {
   a.timed_out_host = h_timeout_dev_;
   a.wait_acc = d_wait_acc_;
   a.phase = d_phase_;
+  if (fused_) a.stop = d_stop_;  // no-op after a converged check (the runs between checks)
   if (direct_) {
     const int64_t rowb = g.pitch * (int64_t)sizeof(float);
     const IpcLayout& me = ipc_lays_[T.rank];
@@ -1786,11 +1822,25 @@ void Engine::device_decide(unsigned long long seq) {
     H2D_NCCL_CHECK(ncclAllReduce(d_resid_, total, 1, ncclDouble, ncclSum, (ncclComm_t)rccl_comm_, compute_));
     launch_decide(total, d, compute_);
   } else if (last_parts_ != nullptr) {  // a lone tile: its units' partials straight to the decision
-    launch_reduce_decide(last_parts_, last_nparts_, d, compute_);
+    if (tiles_[0].spare != nullptr && !tiled_) {
+      // ... made by the next launch's extra block (or flush_pending_decision at the run's end)
+      flush_pending_decision();  // (an older one never consumed: decide it first)
+      pend_parts_ = last_parts_;
+      pend_nparts_ = last_nparts_;
+      pend_dec_ = d;
+    } else {
+      launch_reduce_decide(last_parts_, last_nparts_, d, compute_);
+    }
     last_parts_ = nullptr;
   } else {
     launch_reduce_decide(d_resid_, nt, d, compute_);
   }
+}
+
+void Engine::flush_pending_decision() {
+  if (pend_parts_ == nullptr) return;
+  launch_reduce_decide(pend_parts_, pend_nparts_, pend_dec_, compute_);
+  pend_parts_ = nullptr;
 }
 
 bool Engine::check_point(int64_t steps_before, int k, int lvl) {

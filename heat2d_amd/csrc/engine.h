@@ -464,6 +464,13 @@ class Engine {
   bool decided_in_launch_ = false;        // the last check launch already made the decision
   const double* last_parts_ = nullptr;    // a lone tile's residual partials awaiting the decision
   int last_nparts_ = 0;
+  // a lone streaming tile with a spare buffer: the last check's decision rides in the next
+  // launch's extra block (StreamArgs::pend); its partials alternate between two sets
+  const double* pend_parts_ = nullptr;
+  int pend_nparts_ = 0;
+  DecideArgs pend_dec_{};
+  int pset_ = 0;
+  void flush_pending_decision();
   DecideArgs decide_args(int t, bool decide) const;
   void device_decide(unsigned long long seq);
   bool check_point(int64_t steps_before, int k, int lvl = 0);

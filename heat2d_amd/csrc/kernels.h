@@ -141,8 +141,12 @@ struct StreamDyn {
   // halo counts this launch's halo units wait for, per direction (Dir: N, S, W, E, NW, NE, SW, SE)
   unsigned long long need[kNumDirs] = {};
   unsigned long long copies_need = 0;  // serial pipeline: exchange copy blocks completed before this launch
-  unsigned long long seq = 0;          // check number of a deciding residual launch (DecideArgs::seq)
+  // check number of a deciding residual launch (DecideArgs::seq), or of the pending decision
+  // the launch's extra block makes (StreamArgs::pend: a lone tile, whose launches never decide
+  // in-launch)
+  unsigned long long seq = 0;
   int nunits = 0;                      // == the block's nunits (the launcher's grid size)
+  bool pend = false;                   // == (the block's pend != nullptr): one more block
   unsigned btag = 0;                   // the block's ArgHead::btag
 };
 // The kernel receives the per-launch scalars as separate scalar kernel arguments, read once at the
@@ -210,6 +214,13 @@ struct StreamArgs {
   const unsigned long long* stop = nullptr;
   float* keep = nullptr;
   DecideArgs dec;  // residual launches of a single-tile run: fused sum + decision
+  // Deferred decision of a lone tile's previous check (as TileArgs::pend): one extra block
+  // (blockIdx (nunits + 3) / 4) sums the `pend_n` partials at `pend` and decides (pend_dec; its
+  // seq: the launch's seq argument) while the units compute speculatively into a buffer that is
+  // not the check's input.
+  const double* pend = nullptr;
+  int pend_n = 0;
+  DecideArgs pend_dec;
   int rel = 0;  // signal release: 0 system scope, 1 agent scope, 2 drain only (payload in uncached memory)
   int acq = 0;  // halo-wait acquire: 0 system scope, 1 agent scope, 2 compiler ordering only
   // Output row stores: 0 plain (write-back L2), 1 write-through (buffer_store sc1: the line
@@ -300,6 +311,11 @@ struct PStreamArgs {
   unsigned int* timed_out = nullptr;
   unsigned int* timed_out_host = nullptr;
   unsigned long long* wait_acc = nullptr;
+  // Fused convergence: a launch that starts with *stop != 0 (a converged check before it) does
+  // nothing at all.  Every rank decides the same check identically before its next launch, so
+  // all ranks skip the same launches; the flags and counters they would have bumped are reset
+  // by the re-prime that a converged run needs anyway.
+  const unsigned long long* stop = nullptr;
   // Diagnostics (usually null; recorded only by a build of pstream_kernel.hpp with
   // -DH2D_PSTREAM_PHASES): s_memrealtime ticks (100 MHz) summed over waves and chunks, per
   // phase of a chunk — [0] chunks, [1] chunk-start drain of the previous chunk's stores, [2]

@@ -532,8 +532,10 @@ void launch_stream(const StreamArgs* blk, const StreamArgs& a, const StreamDyn& 
                    bool residual, hipStream_t s) {
   if (a.nunits <= 0) return;
   if (lead_cols(K) != a.R || kWaveCols - 2 * a.R != a.wout) throw std::invalid_argument("launch_stream: R/wout mismatch");
-  if (blk == nullptr || d.nunits != a.nunits || d.btag != a.head.btag)
+  if (blk == nullptr || d.nunits != a.nunits || d.btag != a.head.btag || d.pend != (a.pend != nullptr))
     throw std::invalid_argument("launch_stream: the launch does not name its argument block");
+  if (a.pend != nullptr && (a.dec.ticket != nullptr || a.pend_n <= 0 || a.pend_dec.stop == nullptr))
+    throw std::invalid_argument("launch_stream: a pending decision needs a launch that does not decide itself");
   const bool f32 = precision == kFp32;
   switch (K) {
 #define H2D_CASE(KK) case KK: launch_stream_k<KK>(blk, d, a.wt != 0, f32, residual, s); break;

@@ -461,6 +461,8 @@ __global__ __launch_bounds__(256) void pstream_kernel(const PStreamArgs* __restr
     if (lane == 0) report_timeout(gp(a.timed_out), gp(a.timed_out_host), kIntegArgs);
     return;
   }
+  if (gp(a.stop) != nullptr && __hip_atomic_load(gp(a.stop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull)
+    return;  // converged earlier in this run (PStreamArgs::stop)
   const PUnit* pu = gp(a.units) + w;
   const Unit u = pu->u;
   PSlot sl;

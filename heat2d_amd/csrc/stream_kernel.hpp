@@ -486,6 +486,30 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Sum over the wave, every lane gets it: DPP within each 16-lane row (quad swaps, then row
+// rotations by 4 and 8: no LDS traffic, unlike the ds_bpermute butterfly above), then the four
+// row sums read from lanes 0 / 16 / 32 / 48 and added in that order.  fp64 moves as two halves.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double lane_f64(double v, int lane) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)b, lane);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double dpp_wave_sum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x124>(v);  // row_ror:4
+  v += dpp_f64<0x128>(v);  // row_ror:8
+  return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
+}
+
 template <int K, bool F32, bool RESID, bool WT, int EDGE, bool SIDE, bool HALO>
 __device__ __forceinline__ void run_edge(const float4* rowp, const float4* hrowp, int64_t pitch4, int n,
                                          const LaneCtx& c, const Coef& k, double& racc, bool fixed, int sig_at,
@@ -517,6 +541,21 @@ __device__ __forceinline__ void decide_total(double r, const DecideArgs& d) {
     *gp(d.stop) = d.seq;
     __hip_atomic_store(&gp(d.host)->residual, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&gp(d.host)->stop_seq, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// The deferred decision of a lone tile's previous check (one wave of a launch's extra block,
+// StreamArgs::pend / TileArgs::pend): the partials summed lane-strided, then over the wave.
+__device__ __forceinline__ void decide_pending(const double* parts, int n, DecideArgs pd, unsigned long long seq,
+                                               int lane) {
+  if (__hip_atomic_load(gp(pd.stop), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;  // decided earlier
+  double s = 0.0;
+  for (int i = lane; i < n; i += 64) s += gp(parts)[i];
+  s = dpp_wave_sum(s);
+  if (lane == 0) {
+    pd.seq = seq;
+    *gp(pd.total) = s;
+    decide_total(s, pd);  // the stop word for later launches, the host record
   }
 }
 
@@ -566,7 +605,12 @@ __global__ __launch_bounds__(256) void stream_kernel(const StreamArgs* __restric
   int nunits = a.nunits, nsignal = a.nsignal;
   const unsigned long long* stamps_p = gp(a.stamps);
   asm volatile("" : "+s"(nunits), "+s"(nsignal), "+s"(stamps_p));
-  if (w >= nunits) return;
+  if (w >= nunits) {
+    // the extra block of a launch carrying the previous check's decision (StreamArgs::pend)
+    if (wv == 0 && (int)blockIdx.x == (nunits + 3) / 4 && gp(a.pend) != nullptr)
+      decide_pending(a.pend, a.pend_n, a.pend_dec, seq, (int)(threadIdx.x & 63));
+    return;
+  }
   const int lane = (int)(threadIdx.x & 63);
   const bool stamping = stamps_p != nullptr;  // diagnostics: per-wave timeline
   const unsigned long long t_start = stamping ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -791,7 +835,7 @@ __global__ __launch_bounds__(256) void stream_kernel(const StreamArgs* __restric
         if ((xpushes >> i) & 1) __hip_atomic_fetch_add(gp(a.xsig[i]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if constexpr (RESID) {
-    racc = wave_sum(racc);
+    racc = dpp_wave_sum(racc);
     int slot = w + a.prot;
     if (slot >= a.nunits) slot -= a.nunits;
     DecideArgs dec = a.dec;
@@ -828,7 +872,8 @@ __global__ __launch_bounds__(256) void stream_kernel(const StreamArgs* __restric
 // build/gen/stream_k<K>_f<F32>r<RESID>.hip), so the 44 stencil objects compile in parallel.
 template <int K, bool F32, bool RESID>
 void launch_stream_kv(const StreamArgs* blk, const StreamDyn& d, bool wt, hipStream_t s) {
-  const int blocks = std::max(1, (d.nunits + 3) / 4);  // nunits == 0: a no-op launch (warm_kernels)
+  // nunits == 0: a no-op launch (warm_kernels); a pending decision: one more (deciding) block
+  const int blocks = std::max(1, (d.nunits + 3) / 4 + (d.pend ? 1 : 0));
   StreamNeed need;
   for (int i = 0; i < kNumDirs; ++i) need.v[i] = d.need[i];
   void (*fn)(const StreamArgs*, unsigned long long, unsigned long long, unsigned long long, unsigned, StreamNeed) =

@@ -56,46 +56,6 @@ __device__ __forceinline__ void lds_put(float* p, const float (&v)[CPL]) {
   else *p = v[0];
 }
 
-// Sum over the wave, every lane gets it: DPP within each 16-lane row (quad swaps, then row
-// rotations by 4 and 8: no LDS traffic, unlike the ds_bpermute butterfly), then the four row
-// sums read from lanes 0 / 16 / 32 / 48 and added in that order.  fp64 moves as two 32-bit halves.
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double lane_f64(double v, int lane) {
-  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)b, lane);
-  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ double dpp_wave_sum(double v) {
-  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f64<0x124>(v);  // row_ror:4
-  v += dpp_f64<0x128>(v);  // row_ror:8
-  return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
-}
-
-// The deferred decision of the previous launch's check (one wave of the deciding block): the
-// partials summed lane-strided, then over the wave; the stop word and the host record.
-__device__ __forceinline__ void decide_pending(const TileArgs& a, unsigned long long pend_seq, int lane) {
-  const unsigned long long* stop = gp(a.pend_dec.stop);
-  if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;  // decided earlier
-  double s = 0.0;
-  for (int i = lane; i < a.pend_n; i += 64) s += gp(a.pend)[i];
-  s = dpp_wave_sum(s);
-  if (lane == 0) {
-    DecideArgs pd = a.pend_dec;
-    pd.seq = pend_seq;
-    *gp(pd.total) = s;
-    decide_total(s, pd);  // the stop word for later launches, the host record
-  }
-}
-
 // One time level of a lane's CPL cells from rows r-1 (N), r (C), r+1 (S).  The west / east
 // neighbours of the group are the adjacent lanes' last / first cell (DPP wave shifts: a region
 // row is RY/CPL consecutive lanes of one wave); the first / last lane of a row reads another
@@ -164,7 +124,8 @@ __global__ __launch_bounds__(NT) void tile_lds_kernel(const TileArgs* __restrict
   if (!live) {
     // the deciding block (grid = ntiles + 1 when `pend`): the previous check's decision, off the
     // tile blocks' critical path (they compute speculatively, see TileArgs::pend)
-    if ((int)blockIdx.x == nt && nt > 0 && gp(a.pend) != nullptr && tid < 64) decide_pending(a, d.pend_seq, tid);
+    if ((int)blockIdx.x == nt && nt > 0 && gp(a.pend) != nullptr && tid < 64)
+      decide_pending(a.pend, a.pend_n, a.pend_dec, d.pend_seq, tid);
     return;
   }
   // unconditional load (a dummy zero word without a stop word): no branch, so no wait here

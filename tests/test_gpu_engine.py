@@ -661,6 +661,52 @@ def test_persistent_direct_row_periodic(native, gpu, rows, K, cols):
     assert np.array_equal(e.download(0), oracle(native, rows, 4096, steps + 2 * K, per=(True, False))["grid"])
 
 
+def _converging_at_60(native, nx, ny, boundary=0, per=(False, False)):
+    """A sensitivity between the residuals of the checks at steps 40 and 60 (check every 20)."""
+    r = [oracle(native, nx, ny, s, boundary, per=per, convergence=True, interval=20, sensitivity=0.0)["residual"]
+         for s in (40, 60)]
+    return 0.5 * (r[0] + r[1])
+
+
+@pytest.mark.parametrize("K,cols", [(6, 256), (5, 128)])
+def test_persistent_fused_convergence_lone(native, gpu, K, cols):
+    """The fused check with the persistent kernel forced on a lone tile: the chunks between checks
+    are persistent launches (no-ops once a check converged), the pending decision is made before
+    each of them; converged step and grid equal the oracle's, and so does a run that never
+    converges."""
+    nx, ny = 256, 1000
+    for sens in (_converging_at_60(native, nx, ny, 1), 0.0):
+        kw = dict(convergence=True, interval=20, sensitivity=sens)
+        ref = oracle(native, nx, ny, 200, 1, **kw)
+        e = native.Engine(nx, ny, boundary=1, tblock=K, device=gpu, small_grid_lds=False, tiled=0, persistent=1,
+                          pstream_cols=cols, halo_timeout_s=5.0, **kw)
+        st = e.run(200)
+        assert e.pstream_launches() >= 1
+        assert st["converged"] == ref["converged"] and st["steps_done"] == ref["steps_done"], (st, ref["steps_done"])
+        assert np.array_equal(e.download(0), ref["grid"])
+
+
+def test_persistent_direct_fused_convergence(native, gpu):
+    """Strong scaling's per-rank shape (direct pipeline, row-periodic self-exchange) with the fused
+    check every 20 steps: persistent launches between the checks, the decision through the IPC
+    all-reduce; stops at the oracle's step with its grid, and continues after a re-prime."""
+    rows, K = 512, 8
+    per = (True, False)
+    kw = dict(convergence=True, interval=20, sensitivity=_converging_at_60(native, rows, 4096, 0, per))
+    e = native.Engine(rows, 4096, periodic_x=True, tblock=K, device=gpu, ranks=[0], transport=native.TRANSPORT_IPC,
+                      halo_timeout_s=5.0, pstream_cols=128, **kw)
+    e.ipc_open([e.ipc_handle()])
+    e.ipc_prime()
+    ref = oracle(native, rows, 4096, 200, per=per, **kw)
+    st = e.run(200)
+    assert e.pstream_launches() >= 1
+    assert st["converged"] and ref["converged"] and st["steps_done"] == ref["steps_done"], (st, ref["steps_done"])
+    assert np.array_equal(e.download(0), ref["grid"])
+    e.ipc_prime()
+    e.run(2 * K)
+    assert np.array_equal(e.download(0), oracle(native, rows, 4096, ref["steps_done"] + 2 * K, per=per)["grid"])
+
+
 def test_persistent_auto_policy(native, gpu):
     """Auto: the persistent kernel only for the direct pipeline's short strips, never for a lone
     tile (there launch per chunk is faster)."""

@@ -214,12 +214,16 @@ def test_gpu_halo_wait_sees_a_late_neighbour(tmp_path):
     assert recs[0]["waits"] > 0 and recs[1]["waits"] > 0
 
 
-def test_gpu_persistent_two_processes(tmp_path):
+@pytest.mark.parametrize("mode", ["plain", "conv"])
+def test_gpu_persistent_two_processes(tmp_path, mode):
     """The persistent kernel on two ranks of the direct pipeline (separate processes, IPC handles
-    carrying each rank's persistent push counts): bit-exact on both ranks, across two runs."""
+    carrying each rank's persistent push counts): bit-exact on both ranks, across two runs.
+    conv: with the fused convergence check — persistent launches between the checks, stop at the
+    oracle's step (the decision through the IPC all-reduce), then continue after a re-prime."""
     import re
 
-    out = _torchrun(2, [os.path.join(ROOT, "tests", "_pstream_ranks_worker.py")], str(tmp_path))
+    out = _torchrun(2, [os.path.join(ROOT, "tests", "_pstream_ranks_worker.py")] + (["conv"] if mode == "conv" else []),
+                    str(tmp_path))
     recs = {d["rank"]: d for d in (json.loads(m) for m in re.findall(r'\{"rank"[^{}]*\}', out))}
     assert set(recs) == {0, 1}, out[-2000:]
     if any("skip" in r for r in recs.values()):

@@ -16,8 +16,13 @@ grids = [(80, 64), (160, 128), (320, 256), (640, 512), (1280, 1024), (2560, 2048
 steps = 1000
 
 
-def timed(**kw):
-    e = n.Engine(device=0, boundary=1, **kw)  # grad semantics (zero ghost ring), as the reference's MPI code
+def timed(direct=False, **kw):
+    if direct:  # one rank's tile of a multi-GPU run: row-periodic self-exchange, direct IPC pipeline
+        e = n.Engine(device=0, periodic_x=True, ranks=[0], transport=n.TRANSPORT_IPC, halo_timeout_s=5.0, **kw)
+        e.ipc_open([e.ipc_handle()])
+        e.ipc_prime()
+    else:
+        e = n.Engine(device=0, boundary=1, **kw)  # grad semantics (zero ghost ring), as the reference's MPI code
     e.run(200)
     best = 1e9
     for _ in range(3):
@@ -47,3 +52,12 @@ for nx, ny in grids:
     t2, _ = timed(nx=nx, ny=ny, fused_check=0, **conv)
     print(f"| {nx}x{ny} | {t0:.3e} | {t1:.3e} | {100 * (t1 / t0 - 1):+.1f} % | {t2:.3e} | {100 * (t2 / t0 - 1):+.1f} % "
           f"| {path} |", flush=True)
+# multi-rank rows (one GPU): a rank's tile of 4096^2 over 8 / 4 GPUs through the direct pipeline in a
+# row-periodic self-exchange (the decision through the IPC all-reduce; persistent launches between checks)
+for nx, ny, K in ((512, 4096, 8), (1024, 4096, 8)):
+    t0, path = timed(direct=True, nx=nx, ny=ny, tblock=K)
+    conv = dict(convergence=True, interval=20, sensitivity=0.0)
+    t1, _ = timed(direct=True, nx=nx, ny=ny, tblock=K, **conv)
+    t2, _ = timed(direct=True, nx=nx, ny=ny, tblock=K, fused_check=0, **conv)
+    print(f"| {nx}x{ny} rank tile, direct | {t0:.3e} | {t1:.3e} | {100 * (t1 / t0 - 1):+.1f} % | {t2:.3e} | "
+          f"{100 * (t2 / t0 - 1):+.1f} % | {path} |", flush=True)
