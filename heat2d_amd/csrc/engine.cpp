@@ -1,5 +1,6 @@
 // heat2d_amd — native solver engine (see engine.h).
 #include "engine.h"
+#include "collectives.h"
 
 #include <rccl/rccl.h>
 
@@ -844,7 +845,14 @@ void Engine::launch_chunk_tile(int t, int K, bool residual, int which, int src, 
   if (to_spare) std::swap(tl.spare, tl.buf[1 - src]);  // the check's input becomes the spare
   if (a.waves_done != nullptr) waves_need_ += (unsigned long long)a.nunits;
   progress_tick(ls);
-  if (residual && whole && !lone) reduce_tile_residual(t, K);
+  // the direct pipeline's one tile: its partials go straight into the check's IPC all-reduce
+  // (device_decide), one kernel instead of a reduction and an all-reduce
+  const bool fold = fused_ && direct_ && tiles_.size() == 1;
+  if (residual && whole && !lone && !fold) reduce_tile_residual(t, K);
+  if (residual && whole && fold) {
+    last_parts_ = a.partials;
+    last_nparts_ = L.n_all;
+  }
   if (residual && whole && lone) {
     last_parts_ = a.partials;
     last_nparts_ = L.n_all;
@@ -1813,11 +1821,20 @@ void Engine::device_decide(unsigned long long seq) {
   d.seq = seq;
   if (direct_) {
     ++ipc_resid_epoch_;
-    launch_ipc_allreduce(d_resid_, total, d_ipc_blocks_, tiles_[0].rank, (int)ipc_blocks_.size(),
-                         (int)(ipc_resid_epoch_ & 1), (unsigned long long)ipc_blocks_.size() * ipc_resid_epoch_,
-                         ipc_lays_[tiles_[0].rank].resid_count, ipc_lays_[tiles_[0].rank].resid_slots, kIpcMaxRanks,
-                         std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6)), d_sig_timeout_,
-                         h_timeout_dev_, d_stop_, &d, compute_);
+    const IpcLayout& me = ipc_lays_[tiles_[0].rank];
+    const long long polls = std::max<long long>(1000, (long long)(opt_.halo_timeout_s * 1e6));
+    const unsigned long long target = (unsigned long long)ipc_blocks_.size() * ipc_resid_epoch_;
+    if (last_parts_ != nullptr) {  // the check launch's partials: summed by the all-reduce itself
+      launch_ipc_allreduce_parts(last_parts_, last_nparts_, d_resid_, total, d_ipc_blocks_, tiles_[0].rank,
+                                 (int)ipc_blocks_.size(), (int)(ipc_resid_epoch_ & 1), target, me.resid_count,
+                                 me.resid_slots, kIpcMaxRanks, polls, d_sig_timeout_, h_timeout_dev_, d_stop_, d,
+                                 compute_);
+      last_parts_ = nullptr;
+    } else {
+      launch_ipc_allreduce(d_resid_, total, d_ipc_blocks_, tiles_[0].rank, (int)ipc_blocks_.size(),
+                           (int)(ipc_resid_epoch_ & 1), target, me.resid_count, me.resid_slots, kIpcMaxRanks, polls,
+                           d_sig_timeout_, h_timeout_dev_, d_stop_, &d, compute_);
+    }
   } else if (rccl_comm_) {
     H2D_NCCL_CHECK(ncclAllReduce(d_resid_, total, 1, ncclDouble, ncclSum, (ncclComm_t)rccl_comm_, compute_));
     launch_decide(total, d, compute_);

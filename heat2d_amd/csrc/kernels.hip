@@ -3,6 +3,7 @@
 // itself lives in stream_kernel.hpp, instantiated per (K, precision, residual) in generated TUs.
 // Compiled with -ffp-contract=off.
 #include "stream_kernel.hpp"
+#include "collectives.h"
 
 #include <algorithm>
 #include <atomic>
@@ -114,17 +115,24 @@ __global__ __launch_bounds__(64) void wait_counter_kernel(const unsigned long lo
 // uncached memory), release, bump every block's counter, wait (bounded) until mine shows all
 // contributions of this epoch, then sum the slots in rank order — the same order on every
 // rank, so every rank gets the same bits.
-__global__ __launch_bounds__(64) void ipc_allreduce_kernel(const double* local, double* out, char* const* blocks,
+__global__ __launch_bounds__(64) void ipc_allreduce_kernel(double* local, double* out, char* const* blocks,
                                                            int me, int nr, int parity, unsigned long long target,
                                                            unsigned long long count_off, unsigned long long slot_off,
                                                            int max_ranks, long long max_polls, unsigned int* timed_out,
                                                            unsigned int* timed_out_host,
                                                            const unsigned long long* stop, DecideArgs d,
-                                                           int decide) {
-  if (threadIdx.x != 0) return;
+                                                           int decide, const double* parts, int nparts) {
   // after a converged check no rank contributes any more (each stops on its own schedule)
   if (stop != nullptr && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;
-  const unsigned long long v = __double_as_longlong(*local);
+  double mine = 0.0;
+  if (parts != nullptr) {
+    // this rank's partials first, in one fixed order (lane-strided over one wave, then the wave)
+    for (int i = threadIdx.x; i < nparts; i += 64) mine += parts[i];
+    mine = wave_sum(mine);
+  }
+  if (threadIdx.x != 0) return;
+  if (parts != nullptr) *local = mine;
+  const unsigned long long v = __double_as_longlong(parts != nullptr ? mine : *local);
   for (int r = 0; r < nr; ++r) {
     unsigned long long* slot = reinterpret_cast<unsigned long long*>(blocks[r] + slot_off) + parity * max_ranks + me;
     __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -784,9 +792,21 @@ void launch_ipc_allreduce(const double* local, double* out, char* const* d_block
                           const unsigned long long* stop, const DecideArgs* decide, hipStream_t s) {
   DecideArgs d;
   if (decide) d = *decide;
+  hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(1), dim3(64), 0, s, const_cast<double*>(local), out, d_blocks, me,
+                     nranks, parity, target, (unsigned long long)count_off, (unsigned long long)slot_off, max_ranks,
+                     max_polls, timed_out, timed_out_host, stop, d, decide ? 1 : 0, nullptr, 0);
+  H2D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_ipc_allreduce_parts(const double* parts, int nparts, double* local, double* out, char* const* d_blocks,
+                                int me, int nranks, int parity, unsigned long long target, size_t count_off,
+                                size_t slot_off, int max_ranks, long long max_polls, unsigned int* timed_out,
+                                unsigned int* timed_out_host, const unsigned long long* stop, const DecideArgs& decide,
+                                hipStream_t s) {
+  if (parts == nullptr || nparts <= 0) throw std::invalid_argument("launch_ipc_allreduce_parts: no partials");
   hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(1), dim3(64), 0, s, local, out, d_blocks, me, nranks, parity, target,
                      (unsigned long long)count_off, (unsigned long long)slot_off, max_ranks, max_polls, timed_out,
-                     timed_out_host, stop, d, decide ? 1 : 0);
+                     timed_out_host, stop, decide, 1, parts, nparts);
   H2D_HIP_CHECK(hipGetLastError());
 }
 

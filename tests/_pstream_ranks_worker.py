@@ -3,7 +3,8 @@ strips through the direct IPC pipeline with the persistent kernel on both ranks 
 both launches' waves fit on the GPU together); every rank's tile is compared with the oracle.
 Argument `conv`: with the fused convergence check every 20 steps (the chunks between checks are
 persistent launches, the decision goes through the IPC all-reduce); the run must stop at the
-oracle's step with the oracle's grid, and continue after a re-prime."""
+oracle's step with the oracle's grid; after a re-prime the next run converges again at that
+step (it starts on the converged check's step) with the same grid."""
 import json
 import os
 import sys
@@ -70,11 +71,13 @@ def where(got, ref):
 
 bad1 = where(got, ref)
 dist.barrier()
-e.run(2 * K)
+st2 = e.run(2 * K)
 e.synchronize()
-ref2 = n.oracle_run(nx, ny, steps + 2 * K)["grid"][g["gx0"]:g["gx0"] + g["xcell"], :]
+ref2 = ref if conv else n.oracle_run(nx, ny, steps + 2 * K)["grid"][g["gx0"]:g["gx0"] + g["xcell"], :]
 got2 = e.download(0)
 ok2 = bool(np.array_equal(got2, ref2))
+if conv:
+    ok2 = ok2 and bool(st2["converged"]) and st2["steps_done"] == steps
 print(json.dumps({"rank": rank, "ok": ok, "ok2": ok2, "launches": e.pstream_launches(),
                   "steps_done": int(e.steps_done())}), flush=True)
 if not (ok and ok2):
