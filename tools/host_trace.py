@@ -17,24 +17,28 @@ import time
 def run(n=4096, steps=20, reps=50):
     sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
     import heat2d_amd  # noqa: F401  (kernel-argument default)
+    import torch
     from heat2d_amd._native import native
     nat = native()
-    e = nat.Engine(n, n, boundary=0, precision=0, tblock=7, device=0, small_grid_lds=False)
-    for _ in range(200):
-        e.run(steps)
-    e.synchronize()
-    sub, tot = [], []
-    for _ in range(reps):
-        e.synchronize()
-        t0 = time.perf_counter()
-        e.run(steps)
-        t1 = time.perf_counter()
-        e.synchronize()
-        t2 = time.perf_counter()
-        sub.append((t1 - t0) * 1e6)
-        tot.append((t2 - t0) * 1e6)
-    print(f"{n}x{n} {steps} steps x {reps}: submit median {statistics.median(sub):.1f} us, "
-          f"total median {statistics.median(tot):.1f} us ({statistics.median(tot) / steps:.3f} us/step)")
+    for mode in (2, 3, 0, 1):
+        for st in (1, steps):
+            e = nat.Engine(n, n, boundary=0, precision=0, tblock=7, device=0, small_grid_lds=False, sync_mode=mode)
+            for _ in range(200):
+                e.run(st)
+            e.synchronize()
+            tot, tt = [], []
+            for _ in range(reps):
+                e.synchronize()
+                t0 = time.perf_counter()
+                r = e.run(st)
+                t1 = time.perf_counter()
+                torch.cuda.synchronize()  # the bench's own end (a no-op wait: the run already waited)
+                t2 = time.perf_counter()
+                tot.append((t1 - t0) * 1e6)
+                tt.append((t2 - t0) * 1e6)
+            del e
+            print(f"{n}x{n} sync_mode {mode} {st:3d} steps x {reps}: run() median {statistics.median(tot):7.1f} us, "
+                  f"+ torch sync {statistics.median(tt):7.1f} us ({statistics.median(tt) / st:.3f} us/step)", flush=True)
 
 
 def timeline(db, last=60):

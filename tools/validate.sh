@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 validation on one GPU box: smoke, the whole GPU suite, the bench (20 / 1000 steps), its
+# Validation on one GPU box: smoke, the whole GPU suite, the bench (20 / 1000 steps), its
 # kernel trace, the small-grid check trace, and an A/B of the stencil's integrity checks.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
