@@ -52,8 +52,12 @@ struct EngineOptions {
   double cx = kCxDouble, cy = kCxDouble;
   int tblock = 8;          // max fused steps per chunk (= halo depth)
   int rows_per_wave = 0;   // H; 0 = automatic
-  double edge_weight = 1.2;      // relative cost of a column-edge work unit (load balance)
-  double row_edge_weight = -1.0;  // ... of a row-edge unit (<= 0: edge_weight)
+  // relative cost per row of a column-edge / row-edge work unit (load balance).  Measured per
+  // (h + K) against a plain unit, K=7 ref (tools/timeline.py --units, profiles/unit_balance_r5.md):
+  // column edge 1.16 (4096 rows) / 1.21 (2048), row edge 1.23 / 1.30; a corner unit (both)
+  // is sized at max + 0.1 (plan_units)
+  double edge_weight = 1.16;
+  double row_edge_weight = 1.27;  // (<= 0: edge_weight)
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   int boundary_rows = 8;      // rows per halo-dependent work unit (overlap mode; at least K)
   // Signalled pipeline: ONE launch per chunk with the halo-dependent units first; each of them

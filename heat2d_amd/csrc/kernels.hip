@@ -397,6 +397,7 @@ struct RowRange {
   int64_t strip, a, b;  // rows [a, b) of strip
   bool edge;            // costs `w` per row (global-edge masks)
   bool edge_top = false, edge_bot = false;  // first / last unit is an edge unit (global edge rows)
+  bool corner_top = false, corner_bot = false;  // ... of a column-edge strip: both masks (a corner unit)
   bool side = false;    // costs `side_weight` per row (pushes to a W / E neighbour)
 };
 
@@ -414,6 +415,11 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
   auto rows_for = [&](double U, bool edge) { return std::max<int64_t>(1, (int64_t)(edge ? U / w - K : U - K)); };
   auto rows_side = [&](double U) { return std::max<int64_t>(1, (int64_t)(U / ws - K)); };
   auto rows_row_edge = [&](double U) { return std::max<int64_t>(1, (int64_t)(U / wr - K)); };
+  // a corner unit runs the row- AND column-masked body: measured per (h + K) at 4096^2 / 2048x4096,
+  // K=7, relative to a plain unit: column edge 1.16 / 1.21, row edge 1.23 / 1.30, corner 1.29 /
+  // 1.38 (tools/timeline.py --units) — sized as a column-edge unit it was the launch's last wave
+  const double wc = std::max(w, wr) + 0.1;
+  auto rows_corner = [&](double U) { return std::max<int64_t>(1, (int64_t)(U / wc - K)); };
   auto plan = [&](double U, std::vector<Unit>* out) -> int64_t {
     int64_t count = 0;
     auto emit = [&](int64_t strip, int64_t a, int64_t b, int64_t target) {
@@ -432,7 +438,7 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
     };
     for (const RowRange& r : ranges) {
       int64_t a = r.a, b = r.b;
-      const int64_t he = rows_row_edge(U);
+      const int64_t he = rows_row_edge(U), hc = rows_corner(U);
       if (r.edge_top && b > a) {
         const int64_t e = std::min(b, a + he);
         emit(r.strip, a, e, he);
@@ -441,6 +447,16 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
       if (r.edge_bot && b > a) {
         const int64_t e = std::max(a, b - he);
         emit(r.strip, e, b, he);
+        b = e;
+      }
+      if (r.corner_top && b > a) {
+        const int64_t e = std::min(b, a + hc);
+        emit(r.strip, a, e, hc);
+        a = e;
+      }
+      if (r.corner_bot && b > a) {
+        const int64_t e = std::max(a, b - hc);
+        emit(r.strip, e, b, hc);
         b = e;
       }
       emit(r.strip, a, b, r.side ? rows_side(U) : rows_for(U, r.edge));
@@ -507,6 +523,8 @@ UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, boo
       r.side = (side_w && S.lo < side_cols) || (side_e && S.hi > g.ycell - side_cols);
       r.edge_top = !col_edge && !r.side && row_edge_top;
       r.edge_bot = !col_edge && !r.side && row_edge_bot;
+      r.corner_top = col_edge && !r.side && row_edge_top;
+      r.corner_bot = col_edge && !r.side && row_edge_bot;
       in_r.push_back(r);
     } else {
       in_r.push_back(RowRange{s, top, bot, col_edge});

@@ -5,6 +5,7 @@ time (ready -> end) by unit class, launch span, and the gap to the next launch â
 the per-launch fixed cost that ``profiles/launch_cost_r2.md`` could only fit as one number.
 
 Usage: python tools/timeline.py ROWSxCOLS:K[:steps][:alone|direct|direct2d[:opt=value...]] ... [--json out.json]
+       [--units]  (with --json: every unit's raw stamps and geometry, for per-XCD / per-position analysis)
   direct = the tile row-periodic through the IPC direct pipeline (its own neighbour);
   direct2d = periodic in both dimensions (its own neighbour in all eight directions).
 """
@@ -78,6 +79,9 @@ def run_case(n, spec):
     for Kc, st in tl:
         units = e.unit_list(0, Kc, 3 if direct else 0)
         s = summarize(Kc, st, units)
+        if "--units" in sys.argv:  # per-unit raw data: start, ready, end, hw id, and the unit's strip, x0, h, flags
+            s["unit_rows"] = [[int(v) for v in st[i, :4]] + [int(units[i][0]), int(units[i][1]), int(units[i][2]),
+                                                             int(units[i][3])] for i in range(len(st))]
         if prev_last is not None:
             s["gap_from_prev_us"] = float((s["t_first"] - prev_last) * TICK_US)
         prev_last = s["t_last"]
