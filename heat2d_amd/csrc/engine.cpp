@@ -1248,7 +1248,7 @@ void Engine::poll_abort() {
                   ((all & 1) ? "the exchange gate (boundary units never completed) " : "") +
                   ((all & 2) ? "the device-side halo wait (the exchange never landed) " : "") +
                   ((all & 4) ? "the residual all-reduce (a rank never contributed) " : "") +
-                  ((all & 8) ? "the persistent kernel's neighbour wait" : "");
+                  ((all & 8) ? "the persistent kernel's neighbour wait or its halo units' chunk-order wait" : "");
   }
   throw std::runtime_error(broken_why_);
 }
