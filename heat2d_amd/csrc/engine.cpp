@@ -564,9 +564,17 @@ const Engine::UnitLists& Engine::units(int t, int K) {
     // stores): shorter units for them (opt_.side_weight; 8192x4096 2-D periodic tile, us/step at
     // weight 1.0 / 1.15 / 1.25 / 1.35 / 1.5: 19.7 / 17.6 / 16.4 / 16.0 / 16.2, alone 14.2)
     const bool sw = direct_ && (peer[kW] || peer[kNW] || peer[kSW]), se = direct_ && (peer[kE] || peer[kNE] || peer[kSE]);
+    // the strip-end units become the N / S halo units: they start with the halo wait
+    HaloCost hc;
+    if (attempt == 0 && Hq <= 0 && opt_.halo_rows > 0) {
+      hc.n = peer[kN];
+      hc.s = peer[kS];
+      hc.rows = opt_.halo_rows;
+      hc.min_rows = hmin;
+    }
     UnitPlan Q = plan_units(g, K, Hq, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                             ew, std::max<int64_t>(cap / 2, cap - reserve_sig), nullptr, hb,
-                            attempt == 0 ? opt_.row_edge_weight : 1.0, opt_.side_weight, G_, sw, se);
+                            attempt == 0 ? opt_.row_edge_weight : 1.0, opt_.side_weight, G_, sw, se, hc);
     std::map<int, std::pair<int, int>> ends;  // strip -> (top unit, bottom unit) indices
     for (int i = 0; i < (int)Q.interior.size(); ++i) {
       const Unit& u = Q.interior[i];

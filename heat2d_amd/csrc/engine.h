@@ -58,6 +58,9 @@ struct EngineOptions {
   // is sized at max + 0.1 (plan_units)
   double edge_weight = 1.16;
   double row_edge_weight = 1.27;  // (<= 0: edge_weight)
+  // signalled / direct pipelines: the extra cost of a N / S halo unit in rows of a plain unit (its
+  // halo wait: 2048x4096 direct, K=7: 3.4 µs median against 0.9 for other units; 0: none)
+  double halo_rows = 4.0;
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   int boundary_rows = 8;      // rows per halo-dependent work unit (overlap mode; at least K)
   // Signalled pipeline: ONE launch per chunk with the halo-dependent units first; each of them

@@ -82,9 +82,19 @@ struct UnitPlan {
 // row_edge_weight: the cost weight of units whose cone reaches a global edge ROW (<= 0: edge_weight)
 // side_w / side_e: strips whose outputs reach the first / last side_cols columns push them to a
 // W / E neighbour (2-D direct pipeline): their units cost side_weight per row.
+// halo_n / halo_s (no-peer plans whose strip-end units become the N / S halo units of the
+// signalled and direct pipelines): a strip's first / last unit also costs `halo_rows` extra rows
+// (its halo wait before the first row: ~3.3 µs against ~0.9 for other units, tools/timeline.py
+// --units) and never gets fewer than halo_min rows.
+struct HaloCost {
+  bool n = false, s = false;
+  double rows = 0.0;
+  int min_rows = 0;
+};
 UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
                     int64_t capacity, const bool* peer, int hb, double row_edge_weight = -1.0,
-                    double side_weight = 1.0, int side_cols = 0, bool side_w = false, bool side_e = false);
+                    double side_weight = 1.0, int side_cols = 0, bool side_w = false, bool side_e = false,
+                    const HaloCost& halo = HaloCost{});
 // Resident waves of the streaming kernel on `device` (occupancy query × CUs × 4 waves/block).
 int64_t stream_wave_capacity(int K, int precision, int device);
 

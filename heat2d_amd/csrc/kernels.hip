@@ -398,6 +398,7 @@ struct RowRange {
   bool edge;            // costs `w` per row (global-edge masks)
   bool edge_top = false, edge_bot = false;  // first / last unit is an edge unit (global edge rows)
   bool corner_top = false, corner_bot = false;  // ... of a column-edge strip: both masks (a corner unit)
+  bool halo_top = false, halo_bot = false;  // first / last unit is a N / S halo unit (HaloCost)
   bool side = false;    // costs `side_weight` per row (pushes to a W / E neighbour)
 };
 
@@ -406,7 +407,8 @@ struct RowRange {
 // edge unit costs w times more: target cost U -> h = U - K (plain) or U/w - K (edge).
 std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>& strips,
                               const std::vector<RowRange>& ranges, int H, bool fixed, bool per_x, bool per_y,
-                              double edge_weight, int64_t capacity, double row_edge_weight, double side_weight = 1.0) {
+                              double edge_weight, int64_t capacity, double row_edge_weight, double side_weight = 1.0,
+                              const HaloCost& halo = HaloCost{}) {
   // edge units cost more per row: column-edge strips run the column-masked body on every row,
   // row-edge units (their K-cone reaches a global edge row) the row-masked one
   const double w = std::max(1.0, edge_weight);
@@ -420,6 +422,10 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
   // 1.38 (tools/timeline.py --units) — sized as a column-edge unit it was the launch's last wave
   const double wc = std::max(w, wr) + 0.1;
   auto rows_corner = [&](double U) { return std::max<int64_t>(1, (int64_t)(U / wc - K)); };
+  // a halo unit: its strip's weight, plus the rows its halo wait costs
+  auto rows_halo = [&](double U, bool edge) {
+    return std::max<int64_t>(std::max(1, halo.min_rows), (int64_t)((U - halo.rows) / (edge ? w : 1.0) - K));
+  };
   auto plan = [&](double U, std::vector<Unit>* out) -> int64_t {
     int64_t count = 0;
     auto emit = [&](int64_t strip, int64_t a, int64_t b, int64_t target) {
@@ -459,6 +465,16 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
         emit(r.strip, e, b, hc);
         b = e;
       }
+      if (r.halo_top && b > a) {
+        const int64_t hh = rows_halo(U, r.edge), e = std::min(b, a + hh);
+        emit(r.strip, a, e, hh);
+        a = e;
+      }
+      if (r.halo_bot && b > a) {
+        const int64_t hh = rows_halo(U, r.edge), e = std::max(a, b - hh);
+        emit(r.strip, e, b, hh);
+        b = e;
+      }
       emit(r.strip, a, b, r.side ? rows_side(U) : rows_for(U, r.edge));
     }
     return count;
@@ -492,7 +508,7 @@ std::vector<Unit> size_ranges(const TileGeom& g, int K, const std::vector<Strip>
 
 UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, bool per_y, double edge_weight,
                     int64_t capacity, const bool* peer, int hb, double row_edge_weight, double side_weight,
-                    int side_cols, bool side_w, bool side_e) {
+                    int side_cols, bool side_w, bool side_e, const HaloCost& halo) {
   UnitPlan P;
   const std::vector<Strip> strips = strip_layout(g, K, fixed, per_y);
   const int64_t nstrips = (int64_t)strips.size();
@@ -525,13 +541,16 @@ UnitPlan plan_units(const TileGeom& g, int K, int H, bool fixed, bool per_x, boo
       r.edge_bot = !col_edge && !r.side && row_edge_bot;
       r.corner_top = col_edge && !r.side && row_edge_top;
       r.corner_bot = col_edge && !r.side && row_edge_bot;
+      // (a strip end with a halo has a peer there, not a global edge row)
+      r.halo_top = halo.n && !r.side && !row_edge_top;
+      r.halo_bot = halo.s && !r.side && !row_edge_bot;
       in_r.push_back(r);
     } else {
       in_r.push_back(RowRange{s, top, bot, col_edge});
     }
   }
   P.interior = size_ranges(g, K, strips, in_r, H, fixed, per_x, per_y, edge_weight, capacity, row_edge_weight,
-                           side_weight);
+                           side_weight, halo);
   // Boundary units are short (hb rows): they run first, alone, and gate the halo exchange.
   P.boundary = size_ranges(g, K, strips, bd_r, hb, fixed, per_x, per_y, 1.0, capacity, 1.0);
   auto edge_first = [](const Unit& a, const Unit& b) { return (a.flags != 0) > (b.flags != 0); };
