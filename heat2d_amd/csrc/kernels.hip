@@ -110,9 +110,23 @@ __global__ __launch_bounds__(64) void wait_counter_kernel(const unsigned long lo
   report_timeout(timed_out, timed_out_host, 1u);
 }
 
+// One wave's sum of n partials in a fixed order: 8 independent accumulators per lane, so each lane
+// has 8 loads in flight (a single running sum waited for every load in turn: the check's
+// all-reduce kernel took 11 µs for 1018 partials), then the wave sum.
+__device__ __forceinline__ double wave_sum_partials(const double* __restrict__ p, int n, int lane) {
+  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int i = lane; i < n; i += 64 * 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i + 64 * j < n) acc[j] += p[i + 64 * j];
+  }
+  const double s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  return wave_sum(s);
+}
+
 // Scalar all-reduce over the IPC-mapped blocks of every rank (direct transport), one lane:
 // publish my value into slot [parity][me] of every block (system-scope stores to the peers'
-// uncached memory), release, bump every block's counter, wait (bounded) until mine shows all
+// uncached memory), drain them, bump every block's counter, wait (bounded) until mine shows all
 // contributions of this epoch, then sum the slots in rank order — the same order on every
 // rank, so every rank gets the same bits.
 __global__ __launch_bounds__(64) void ipc_allreduce_kernel(double* local, double* out, char* const* blocks,
@@ -124,12 +138,8 @@ __global__ __launch_bounds__(64) void ipc_allreduce_kernel(double* local, double
                                                            int decide, const double* parts, int nparts) {
   // after a converged check no rank contributes any more (each stops on its own schedule)
   if (stop != nullptr && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;
-  double mine = 0.0;
-  if (parts != nullptr) {
-    // this rank's partials first, in one fixed order (lane-strided over one wave, then the wave)
-    for (int i = threadIdx.x; i < nparts; i += 64) mine += parts[i];
-    mine = wave_sum(mine);
-  }
+  // this rank's partials first, in one fixed order
+  const double mine = parts != nullptr ? wave_sum_partials(parts, nparts, (int)threadIdx.x) : 0.0;
   if (threadIdx.x != 0) return;
   if (parts != nullptr) *local = mine;
   const unsigned long long v = __double_as_longlong(parts != nullptr ? mine : *local);
@@ -137,8 +147,9 @@ __global__ __launch_bounds__(64) void ipc_allreduce_kernel(double* local, double
     unsigned long long* slot = reinterpret_cast<unsigned long long*>(blocks[r] + slot_off) + parity * max_ranks + me;
     __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // The slots and counters live in the ranks' uncached (MTYPE UC) IPC blocks: an acknowledged
+  // store is in memory, so draining the slot stores orders them before the counter adds — no
+  // system-scope release (an L2 write-back: the kernel took 11.2 µs with it, profiles/conv_direct_r5.txt)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int r = 0; r < nr; ++r)
     __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(blocks[r] + count_off), 1ull, __ATOMIC_RELAXED,
@@ -152,7 +163,8 @@ __global__ __launch_bounds__(64) void ipc_allreduce_kernel(double* local, double
     }
     __builtin_amdgcn_s_sleep(2);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // (uncached slots, read with system-scope loads: only the compiler must not hoist them above the poll)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const unsigned long long* slots = reinterpret_cast<const unsigned long long*>(blocks[me] + slot_off) + parity * max_ranks;
   double sum = 0.0;
   for (int r = 0; r < nr; ++r)
@@ -165,11 +177,9 @@ __global__ __launch_bounds__(64) void decide_kernel(const double* sum, DecideArg
   if (threadIdx.x == 0) decide_total(*sum, d);
 }
 
-// Deterministic sum of n partials (the same fixed order as publish_partial) + the decision.
+// Deterministic sum of n partials (one fixed order: wave_sum_partials) + the decision.
 __global__ __launch_bounds__(64) void reduce_decide_kernel(const double* __restrict__ in, int n, DecideArgs d) {
-  double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 64) s += in[i];
-  s = wave_sum(s);
+  const double s = wave_sum_partials(in, n, (int)threadIdx.x);
   if (threadIdx.x == 0) {
     *d.total = s;
     decide_total(s, d);
