@@ -126,7 +126,7 @@ __device__ __forceinline__ double wave_sum_partials(const double* __restrict__ p
 
 // Scalar all-reduce over the IPC-mapped blocks of every rank (direct transport), one lane:
 // publish my value into slot [parity][me] of every block (system-scope stores to the peers'
-// uncached memory), drain them, bump every block's counter, wait (bounded) until mine shows all
+// uncached memory), release, bump every block's counter, wait (bounded) until mine shows all
 // contributions of this epoch, then sum the slots in rank order — the same order on every
 // rank, so every rank gets the same bits.
 __global__ __launch_bounds__(64) void ipc_allreduce_kernel(double* local, double* out, char* const* blocks,
@@ -147,9 +147,11 @@ __global__ __launch_bounds__(64) void ipc_allreduce_kernel(double* local, double
     unsigned long long* slot = reinterpret_cast<unsigned long long*>(blocks[r] + slot_off) + parity * max_ranks + me;
     __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // The slots and counters live in the ranks' uncached (MTYPE UC) IPC blocks: an acknowledged
-  // store is in memory, so draining the slot stores orders them before the counter adds — no
-  // system-scope release (an L2 write-back: the kernel took 11.2 µs with it, profiles/conv_direct_r5.txt)
+  // (system-scope release and acquire kept: dropping them, as the halo pushes to the same uncached
+  // blocks do, measured no faster — the kernel's time is its chain of round trips,
+  // profiles/conv_direct_r5.txt — and this path has not yet run across GPUs)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int r = 0; r < nr; ++r)
     __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(blocks[r] + count_off), 1ull, __ATOMIC_RELAXED,
@@ -163,8 +165,7 @@ __global__ __launch_bounds__(64) void ipc_allreduce_kernel(double* local, double
     }
     __builtin_amdgcn_s_sleep(2);
   }
-  // (uncached slots, read with system-scope loads: only the compiler must not hoist them above the poll)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const unsigned long long* slots = reinterpret_cast<const unsigned long long*>(blocks[me] + slot_off) + parity * max_ranks;
   double sum = 0.0;
   for (int r = 0; r < nr; ++r)
