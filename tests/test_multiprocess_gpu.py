@@ -126,6 +126,22 @@ def test_gpu_bench_persistent_rehearsal(tmp_path, n):
     assert len(pl) == n and min(pl) > 0, pl
 
 
+def test_gpu_bench_two_ranks_driver_environment(tmp_path):
+    """The driver's own command at N=2 (default grid, pre-warm and flags) in the driver's environment:
+    no HIP_FORCE_DEV_KERNARG inherited from this test process — bench.py's import of the library
+    picks the kernel-argument setting itself, exactly as in the driver's run."""
+    env = _env()
+    env.pop("HIP_FORCE_DEV_KERNARG", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+           "--warmup", "5"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["steps"] == 20 and d["warmup"] == 5 and d["verified"] is True
+    assert d["config"]["grid"] == [4096, 4096]
+
+
 def test_gpu_bench_two_ranks_ipc(tmp_path):
     """The bench at N=2 on one GPU: the gate picks the direct IPC transport first."""
     out = _torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "40", "--warmup", "8", "--side",
