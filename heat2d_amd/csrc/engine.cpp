@@ -1688,7 +1688,7 @@ const Engine::PPlan* Engine::pplan(int K) {
     const int bpc = pstream_blocks_per_cu(K, opt_.precision, P.cpl);
     P.host = plan_pstream(g, K, opt_.boundary == kFixed, opt_.periodic_x, opt_.periodic_y,
                           opt_.row_edge_weight > 0 ? opt_.row_edge_weight : opt_.edge_weight, cap, halo_n, halo_s,
-                          std::max(K, G_), P.cpl);
+                          std::max(K, G_), P.cpl, opt_.pstream_halo_weight);
     P.n = (int)P.host.size();
     if (P.n == 0 || bpc < 1 || (P.n + 3) / 4 > (int64_t)device_cus_ * bpc) P.n = 0;
     // N / S halo units: each adds 1 to the neighbour's flag per chunk (the neighbours learn the

@@ -61,6 +61,7 @@ struct EngineOptions {
   // signalled / direct pipelines: the extra cost of a N / S halo unit in rows of a plain unit (its
   // halo wait: 2048x4096 direct, K=7: 3.4 µs median against 0.9 for other units; 0: none)
   double halo_rows = 4.0;
+  double pstream_halo_weight = 1.0;  // persistent plans: cost weight of a band with a N / S halo
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   int boundary_rows = 8;      // rows per halo-dependent work unit (overlap mode; at least K)
   // Signalled pipeline: ONE launch per chunk with the halo-dependent units first; each of them

@@ -346,9 +346,11 @@ int pstream_blocks_per_cu(int K, int precision, int cpl);
 void warm_pstream_kernels(int precision, int kmax, hipStream_t s);
 // The aligned unit grid of the persistent kernel (empty if the tile does not allow one):
 // `bands` row bands (even when both halo directions exist), every band at least hmin rows;
-// strips of 64 * cpl columns.
+// strips of 64 * cpl columns.  halo_weight: the cost weight of a band with a N / S halo (its
+// units wait for the neighbour's pushes every chunk; 1: none).
 std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x, bool per_y, double row_edge_weight,
-                                int64_t capacity, bool halo_n, bool halo_s, int hmin, int cpl = 4);
+                                int64_t capacity, bool halo_n, bool halo_s, int hmin, int cpl = 4,
+                                double halo_weight = 1.0);
 
 // Largest K with a compiled streaming kernel.
 constexpr int kMaxK = 16;

@@ -656,7 +656,7 @@ void warm_pstream_kernels(int precision, int kmax, hipStream_t s) {
 }
 
 std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x, bool per_y, double row_edge_weight,
-                                int64_t capacity, bool halo_n, bool halo_s, int hmin, int cpl) {
+                                int64_t capacity, bool halo_n, bool halo_s, int hmin, int cpl, double halo_weight) {
   std::vector<PUnit> out;
   const int64_t W = wave_cols(cpl);
   const std::vector<Strip> strips = strip_layout(g, K, fixed, per_y, cpl);
@@ -681,6 +681,8 @@ std::vector<PUnit> plan_pstream(const TileGeom& g, int K, bool fixed, bool per_x
     const int64_t eq = g.xcell / m;
     if (row_edge(0, eq)) w[0] = wr;
     if (row_edge(g.xcell - eq, g.xcell)) w[m - 1] = wr;
+    if (halo_n) w[0] = std::max(w[0], std::max(1.0, halo_weight));
+    if (halo_s) w[m - 1] = std::max(w[m - 1], std::max(1.0, halo_weight));
     double inv = 0.0;
     for (double x : w) inv += 1.0 / x;
     const double U = ((double)g.xcell + (double)m * K) / inv;

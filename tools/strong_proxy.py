@@ -17,7 +17,7 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 960
 Ks = [int(k) for k in sys.argv[3].split(",")] if len(sys.argv) > 3 else [4, 6, 8, 10, 12, 16]
 cap = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # wave_capacity override (0: occupancy query)
 # extra engine options, "name=value,name=value" (e.g. wt_store=0)
-opts = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in sys.argv[5].split(",") if kv} if len(sys.argv) > 5 else {}
+opts = {kv.split("=")[0]: (float if "." in kv.split("=")[1] else int)(kv.split("=")[1]) for kv in sys.argv[5].split(",") if kv} if len(sys.argv) > 5 else {}
 Ns = [int(v) for v in sys.argv[6].split(",")] if len(sys.argv) > 6 else [1, 2, 4, 8, 16]
 
 
