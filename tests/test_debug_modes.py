@@ -213,7 +213,7 @@ def test_host_sanitizers_engine_cpu_path(native, tmp_path):
 
 def test_kernel_arguments_default_to_host_memory():
     """Importing heat2d_amd selects host-memory kernel arguments for the HIP runtime unless the
-    user chose (docs/ARCHITECTURE.md, "Kernel arguments and metadata memory"), and records the
+    user chose (docs/ARCHITECTURE.md, "Kernel arguments (round 5)"), and records the
     effective state; the CLI does the same, and bench.py runs the library default (no override of
     its own), so the bench times what the tests run.  A fresh interpreter, so the setting is seen
     before anything initialises the GPU."""
@@ -229,6 +229,7 @@ def test_kernel_arguments_default_to_host_memory():
     env["HIP_FORCE_DEV_KERNARG"] = "1"  # the user's choice is kept
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
     assert out.stdout.split()[-2:] == ["1", "False"]
+    assert "device-memory kernel arguments" in out.stderr  # ... with a warning
     with open(os.path.join(root, "bench.py")) as fh:
         assert "HIP_FORCE_DEV_KERNARG" not in fh.read()
     with open(os.path.join(root, "heat2d_amd", "csrc", "heat2d_main.cpp")) as fh:
