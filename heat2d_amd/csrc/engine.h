@@ -61,7 +61,11 @@ struct EngineOptions {
   // signalled / direct pipelines: the extra cost of a N / S halo unit in rows of a plain unit (its
   // halo wait: 2048x4096 direct, K=7: 3.4 µs median against 0.9 for other units; 0: none)
   double halo_rows = 4.0;
-  double pstream_halo_weight = 1.0;  // persistent plans: cost weight of a band with a N / S halo
+  // persistent plans: cost weight of a band with a N / S halo (its units wait for the neighbour's
+  // pushes every chunk).  Strong-scaling proxy, K=8, us/step at 1.0 / 1.1 / 1.15 / 1.2, two rounds:
+  // 512x4096 2.04-2.08 / 1.91-1.93 / 1.84-1.87 / 2.10-2.13; 1024x4096 3.11-3.20 / 3.11-3.12 /
+  // 3.06-3.07 / 3.03-3.04 (profiles/pstream_halo_weight_r5.txt)
+  double pstream_halo_weight = 1.15;
   int64_t wave_capacity = 0;  // resident waves per launch; 0 = occupancy query
   int boundary_rows = 8;      // rows per halo-dependent work unit (overlap mode; at least K)
   // Signalled pipeline: ONE launch per chunk with the halo-dependent units first; each of them
