@@ -59,8 +59,10 @@ struct EngineOptions {
   double edge_weight = 1.16;
   double row_edge_weight = 1.27;  // (<= 0: edge_weight)
   // signalled / direct pipelines: the extra cost of a N / S halo unit in rows of a plain unit (its
-  // halo wait: 2048x4096 direct, K=7: 3.4 µs median against 0.9 for other units; 0: none)
-  double halo_rows = 4.0;
+  // halo wait: 2048x4096 direct, K=7: 3.4 µs median against 0.9 for other units; 0: none).
+  // 2048x4096 direct K=7, us/step, two rounds: 2 rows 5.20 / 5.23, 4 rows 5.21 / 5.24, 6 rows
+  // 5.13 / 5.08 (profiles/halo_rows_r5.txt)
+  double halo_rows = 6.0;
   // persistent plans: cost weight of a band with a N / S halo (its units wait for the neighbour's
   // pushes every chunk).  Strong-scaling proxy, K=8, us/step at 1.0 / 1.1 / 1.15 / 1.2, two rounds:
   // 512x4096 2.04-2.08 / 1.91-1.93 / 1.84-1.87 / 2.10-2.13; 1024x4096 3.11-3.20 / 3.11-3.12 /
