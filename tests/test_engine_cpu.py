@@ -156,3 +156,18 @@ def test_unit_planner_covers_rows_and_packs_rounds(native, n, cap):
     # one full round when possible, otherwise nearly-full rounds
     rounds = -(-len(units) // cap)
     assert len(units) <= cap or len(units) / (rounds * cap) > 0.9
+
+
+def test_unit_planner_sizes_corner_units_by_their_cost(native):
+    """A corner unit (row- and column-masked body) costs more per row than a column-edge unit
+    (profiles/unit_balance_r5.md: it was the launch's last wave when sized like one): the planner
+    gives it fewer rows, and every unit class stays within one resident round."""
+    for n in (4096, 2048):
+        units = native.unit_plan(n, 4096, 7, 0, True, False, False, 1.16, 1024)
+        assert len(units) <= 1024
+        by = {}
+        for _s, _x0, h, flags in units:
+            by.setdefault(flags & 3, []).append(h)
+        assert set(by) == {0, 1, 2, 3}, sorted(by)
+        assert max(by[3]) < min(by[1]) < min(by[0])  # corner < column edge < plain
+        assert max(by[2]) < min(by[0])  # row edge < plain
